@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident RS(6,4) encode+decode throughput on MI355X.
+
+Workload (BASELINE.json configs[1] + configs[2], the metric's "encode+decode"):
+one step = RS(6,4) encode of B=4096 stripes x 64 KiB chunks (1 GiB of data per
+GPU) followed by single-erasure decode of the same batch (data shard 0 lost,
+survivors {1,2,3,4}).  Stripes are independent, so with N GPUs every rank codes
+its own batch (weak scaling, no collective on the data path).
+
+value = data bytes coded by all ranks (k*L per stripe per operation) / the
+slowest rank's time, in GiB/s.  roofline = the encode kernel (dominant launch):
+algorithmic bytes (k+m)*L*B per launch / its mean HIP-event duration, against
+the 8.0 TB/s HBM3E peak.  cpu_baseline = the oracle's ISA-L-algorithm SIMD path
+on the host cores, rank 0 only (test infrastructure, not the product path).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--chunk BYTES] [--stripes B]
+  multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, decimal GB/s (MI355X_MICROARCH.md)
+GIB = float(1 << 30)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--k", type=int, default=4)
+    ap.add_argument("--m", type=int, default=2)
+    ap.add_argument("--chunk", type=int, default=65536)
+    ap.add_argument("--stripes", type=int, default=4096)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target CPU-baseline work time (rank 0, N=1)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (PCIe) measurement")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def pmc_traffic(kernel_substr: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except Exception:
+            continue
+        for name, rec in d.get("kernels", {}).items():
+            if kernel_substr in name:
+                return rec.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    return None, None
+
+
+def cpu_baseline(args, k, m, L):
+    """Oracle SIMD path (ISA-L's algorithm restated) on the host cores; bounded sample."""
+    import numpy as np
+    from oracle import ec_oracle as orc
+    threads = max(1, min(16, os.cpu_count() or 1))
+    stripes = 250  # BASELINE configs[0]: 1000 data chunks of 64 KiB
+    n = k + m
+    rng = np.random.default_rng(0xE1EC7)
+    buf = rng.integers(0, 256, size=(stripes, n, L), dtype=np.uint8)
+    em = orc.cauchy_matrix(k, m)
+    enc_coef = em[k:]
+    rc, dec_coef = orc.decode_matrix(k, m, list(range(1, k + 1)), [0])
+    out = np.empty((stripes, 1, L), np.uint8)
+    level = orc.simd_best()
+    sstride = n * L
+    enc_src = [j * L for j in range(k)]
+    enc_dst = [(k + r) * L for r in range(m)]
+    dec_src = [j * L for j in range(1, k + 1)]
+    # warm, then repeat encode+decode until the time budget is used
+    orc.batch_apply(enc_coef, buf, sstride, enc_src, buf, sstride, enc_dst, L, stripes, threads, level)
+    total_t, reps = 0.0, 0
+    while total_t < args.cpu_seconds or reps < 2:
+        total_t += orc.batch_apply(enc_coef, buf, sstride, enc_src, buf, sstride, enc_dst, L, stripes,
+                                   threads, level)
+        total_t += orc.batch_apply(dec_coef, buf, sstride, dec_src, out, L, [0], L, stripes, threads, level)
+        reps += 1
+    assert np.array_equal(out[:, 0], buf[:, 0]), "CPU baseline decode mismatch"
+    data_bytes = 2 * reps * stripes * k * L
+    return {
+        "value": round(data_bytes / total_t / GIB, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"RS({n},{k}) encode+decode (erase 0), {stripes} stripes x {L} B "
+                  f"({stripes * k} data chunks), {reps} reps, {total_t:.1f} s, "
+                  f"oracle {orc.simd_name(level)} x {threads} threads",
+    }, buf
+
+
+def host_inclusive(coder, k, m, L, stripes_total, dev):
+    """Pinned host -> H2D -> encode -> D2H, two streams; GiB/s of data."""
+    from elect_amd.batch import encode_batch
+    chunk = 256  # stripes per transfer (64 MiB of data at 64 KiB chunks)
+    nchunks = max(2, stripes_total // chunk)
+    h_data = torch.randint(0, 256, (nchunks * chunk, k, L), dtype=torch.uint8).pin_memory()
+    h_par = torch.empty((nchunks * chunk, m, L), dtype=torch.uint8).pin_memory()
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    d_data = [torch.empty((chunk, k, L), dtype=torch.uint8, device=dev) for _ in range(2)]
+    d_par = [torch.empty((chunk, m, L), dtype=torch.uint8, device=dev) for _ in range(2)]
+
+    def run():
+        for c in range(nchunks):
+            s = c % 2
+            with torch.cuda.stream(streams[s]):
+                d_data[s].copy_(h_data[c * chunk:(c + 1) * chunk], non_blocking=True)
+                encode_batch(coder, d_data[s], d_par[s], stream=streams[s])
+                h_par[c * chunk:(c + 1) * chunk].copy_(d_par[s], non_blocking=True)
+        torch.cuda.synchronize()
+
+    run()
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        run()
+    dt = time.perf_counter() - t0
+    return round(reps * nchunks * chunk * k * L / dt / GIB, 2)
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    dev = torch.device("cuda", local if world > 1 else 0)
+    from elect_amd.batch import decode_batch, encode_batch
+    from elect_amd.coder import RSCoder
+
+    k, m, L, B = args.k, args.m, args.chunk, args.stripes
+    n = k + m
+    coder = RSCoder(k, m)
+    g = torch.Generator(device=dev).manual_seed(0xE1EC7 + rank)
+    stripe = torch.empty((B, n, L), dtype=torch.uint8, device=dev)
+    stripe[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g)
+    rebuilt = torch.empty((B, 1, L), dtype=torch.uint8, device=dev)
+    survivors = list(range(1, k + 1))
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        encode_batch(coder, stripe[:, :k], stripe[:, k:], stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        decode_batch(coder, stripe, survivors, [0], rebuilt, inputs_by_unit=True, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(elapsed, world)
+
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    ok = bool(torch.equal(rebuilt[:, 0], stripe[:, 0]))
+
+    data_bytes_per_rank_step = 2 * B * k * L  # encode k*L + decode k*L survivors, per stripe
+    value = world * args.steps * data_bytes_per_rank_step / elapsed / GIB
+    enc_alg = B * n * L               # (k+m)*L per stripe
+    dec_alg = B * (k + 1) * L         # (k+e)*L per stripe, e = 1
+    enc_gbs = enc_alg / (enc_ms * 1e-3) / 1e9
+    dec_gbs = dec_alg / (dec_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic("gf_apply_x16ILi4ELi2E")
+
+    out = {
+        "metric": "GiB/s device-resident RS(6,4) encode+decode, 64 KiB chunks, 1/2/4/8 GPU",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (device-generated uniform random bytes)",
+        "config": {
+            "workload": f"RS({n},{k}) encode + single-erasure decode (erase 0, survivors "
+                        f"{survivors}), {B} stripes x {L} B chunks per GPU "
+                        f"({B * k * L / GIB:.2f} GiB data per op per GPU)",
+            "k": k, "m": m, "chunk_bytes": L, "stripes_per_gpu": B,
+            "parallelism": f"stripe-partitioned x{world}, no collectives",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(enc_gbs, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": "gf_apply_x16<4,2> (encode)",
+            "algorithmic_bytes_per_launch": enc_alg,
+            "traffic_source": traffic_src,
+        },
+        "kernels": {
+            "encode": {"ms": round(enc_ms, 4), "GB/s": round(enc_gbs, 1),
+                       "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
+                       "data_GiB/s": round(B * k * L / (enc_ms * 1e-3) / GIB, 1)},
+            "decode_1erasure": {"ms": round(dec_ms, 4), "GB/s": round(dec_gbs, 1),
+                                "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
+                                "data_GiB/s": round(B * k * L / (dec_ms * 1e-3) / GIB, 1)},
+        },
+        "verified": ok,
+    }
+    if rank == 0 and not args.no_host:
+        out["host_inclusive_GiB/s"] = host_inclusive(coder, k, m, L, min(B, 1024), dev)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cb, _ = cpu_baseline(args, k, m, L)
+        out["cpu_baseline"] = cb
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

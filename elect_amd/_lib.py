@@ -1,0 +1,130 @@
+"""ctypes binding of libelect_ec.so (the C ABI in include/elect_ec.h).
+
+There is no CPU fallback anywhere in this package: if the library is missing
+this module raises at import, and without a GPU the compute entry points return
+ELECT_EC_ENODEV, which is raised as ECDeviceError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libelect_ec.so")
+
+OK = 0
+WARN_SINGULAR = 1
+EINVAL = -1
+ESINGULAR = -2
+EDEVICE = -3
+ENOMEM = -4
+ENODEV = -5
+
+DECODE_COMPAT = 0
+DECODE_STRICT = 1
+INPUTS_BY_UNIT = 1
+OUTPUTS_BY_UNIT = 2
+
+MAX_DATA_UNITS = 10
+MAX_UNITS = 14
+MAX_APPLY = 16
+
+
+class ECError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        super().__init__(f"{what}: {strerror(status)} ({status})" if what else strerror(status))
+
+
+class ECDeviceError(ECError):
+    pass
+
+
+class ECSingularError(ECError):
+    pass
+
+
+class ECInvalidArgument(ECError, ValueError):
+    pass
+
+
+class Shards(ctypes.Structure):
+    _fields_ = [("base", ctypes.c_void_p), ("stripe_stride", ctypes.c_size_t),
+                ("shard_stride", ctypes.c_size_t)]
+
+
+class ColumnT(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("stripe_stride", ctypes.c_size_t)]
+
+
+_u8p = ctypes.POINTER(ctypes.c_ubyte)
+_u8pp = ctypes.POINTER(ctypes.c_void_p)
+_ip = ctypes.POINTER(ctypes.c_int)
+_cp = ctypes.c_void_p
+
+# (name, restype, argtypes) for every symbol include/elect_ec.h declares.
+SIGNATURES = [
+    ("elect_ec_version", ctypes.c_char_p, []),
+    ("elect_ec_strerror", ctypes.c_char_p, [ctypes.c_int]),
+    ("elect_ec_device_count", ctypes.c_int, [_ip]),
+    ("elect_ec_coder_create", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_cp)]),
+    ("elect_ec_coder_destroy", None, [_cp]),
+    ("elect_ec_coder_num_data_units", ctypes.c_int, [_cp]),
+    ("elect_ec_coder_num_parity_units", ctypes.c_int, [_cp]),
+    ("elect_ec_coder_encode_matrix", ctypes.c_int, [_cp, _u8p, ctypes.c_size_t]),
+    ("elect_ec_coder_gf_tables", ctypes.c_int, [_cp, _u8p, ctypes.c_size_t]),
+    ("elect_ec_coder_decode_matrix", ctypes.c_int, [_cp, _ip, _ip, ctypes.c_int, ctypes.c_int, _u8p]),
+    ("elect_ec_encode", ctypes.c_int, [_cp, _u8pp, _u8pp, ctypes.c_size_t]),
+    ("elect_ec_encode_update", ctypes.c_int, [_cp, _u8pp, ctypes.c_int, _u8pp, ctypes.c_size_t]),
+    ("elect_ec_decode", ctypes.c_int, [_cp, _u8pp, _ip, _ip, ctypes.c_int, _u8pp, ctypes.c_size_t,
+                                       ctypes.c_int]),
+    ("elect_ec_encode_batch", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, Shards, Shards, _cp]),
+    ("elect_ec_decode_batch", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, Shards, _ip, _ip,
+                                             ctypes.c_int, Shards, ctypes.c_uint, ctypes.c_int, _cp]),
+    ("elect_ec_encode_update_batch", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                                                    ColumnT, ColumnT, Shards, Shards, _cp]),
+    ("elect_ec_apply_batch", ctypes.c_int, [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                                            ctypes.c_size_t, ctypes.POINTER(ColumnT),
+                                            ctypes.POINTER(ColumnT), _cp]),
+]
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} is missing: build the MI355X engine first "
+                      "(python -m elect_amd.build) — there is no CPU fallback")
+
+lib = ctypes.CDLL(LIB_PATH)
+for _name, _res, _args in SIGNATURES:
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+def strerror(status: int) -> str:
+    return lib.elect_ec_strerror(status).decode()
+
+
+def check(status: int, what: str = "") -> int:
+    """Raise for negative statuses; pass OK / WARN_SINGULAR through."""
+    if status >= 0:
+        return status
+    if status in (ENODEV, EDEVICE, ENOMEM):
+        raise ECDeviceError(status, what)
+    if status == ESINGULAR:
+        raise ECSingularError(status, what)
+    if status == EINVAL:
+        raise ECInvalidArgument(status, what)
+    raise ECError(status, what)
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    lib.elect_ec_device_count(ctypes.byref(n))
+    return n.value
+
+
+def ptr_array(addrs) -> ctypes.Array:
+    return (ctypes.c_void_p * max(1, len(addrs)))(*addrs)
+
+
+def int_array(xs) -> ctypes.Array:
+    return (ctypes.c_int * max(1, len(xs)))(*[int(x) for x in xs])

@@ -1,0 +1,99 @@
+"""Device-resident batched API over torch tensors (PyTorch is only the
+allocator and stream provider here; every byte is coded by libelect_ec.so).
+
+Layout convention: a batch is a uint8 tensor shaped [stripes, shards, L] (any
+strides on the first two dims, contiguous last dim) on a HIP device.  A shard
+row s,i starts at data_ptr + s*stride(0) + i*stride(1).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import ColumnT, Shards, check, int_array, lib
+from .coder import RSCoder
+
+
+def _shards(t: torch.Tensor) -> Shards:
+    if t.dtype != torch.uint8 or t.dim() != 3 or t.stride(2) != 1:
+        raise ValueError("expected a uint8 [stripes, shards, L] tensor with a contiguous last dim")
+    if t.device.type != "cuda":
+        raise ValueError("device-resident API needs a HIP (cuda) tensor")
+    return Shards(t.data_ptr(), t.stride(0), t.stride(1))
+
+
+def _column(t: torch.Tensor) -> ColumnT:
+    if t.dtype != torch.uint8 or t.dim() != 2 or t.stride(1) != 1 or t.device.type != "cuda":
+        raise ValueError("expected a uint8 [stripes, L] HIP tensor with a contiguous last dim")
+    return ColumnT(t.data_ptr(), t.stride(0))
+
+
+def _stream(stream) -> int:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream
+
+
+def encode_batch(coder: RSCoder, data: torch.Tensor, parity: torch.Tensor, stream=None) -> None:
+    """parity[s, r] = XOR_j E[k+r][j] * data[s, j] for every stripe s (stream ordered)."""
+    B, k, L = data.shape
+    if k != coder.k or parity.shape[0] != B or parity.shape[1] != coder.m or parity.shape[2] != L:
+        raise ValueError(f"shape mismatch: data {tuple(data.shape)} parity {tuple(parity.shape)}")
+    check(lib.elect_ec_encode_batch(coder.handle, L, B, _shards(data), _shards(parity), _stream(stream)),
+          "encode_batch")
+
+
+def decode_batch(coder: RSCoder, inputs: torch.Tensor, decode_indexes, erased, outputs: torch.Tensor,
+                 mode: int = _lib.DECODE_COMPAT, inputs_by_unit: bool = False,
+                 outputs_by_unit: bool = False, stream=None) -> int:
+    """Reconstruct `erased` units of every stripe from k survivors.
+
+    inputs: [B, k, L] survivors in decode_indexes order, or (inputs_by_unit)
+    a [B, k+m, L] stripe tensor read at rows decode_indexes.  outputs: [B, e, L],
+    or (outputs_by_unit) the stripe tensor, written at rows erased."""
+    B, _, L = inputs.shape
+    flags = (_lib.INPUTS_BY_UNIT if inputs_by_unit else 0) | (_lib.OUTPUTS_BY_UNIT if outputs_by_unit else 0)
+    if len(decode_indexes) != coder.k:
+        raise ValueError("decode_indexes needs exactly k entries")
+    return check(lib.elect_ec_decode_batch(coder.handle, L, B, _shards(inputs), int_array(decode_indexes),
+                                           int_array(erased), len(erased), _shards(outputs), flags, mode,
+                                           _stream(stream)), "decode_batch")
+
+
+def encode_update_batch(coder: RSCoder, target: int, old: torch.Tensor, new: torch.Tensor,
+                        parity_in: torch.Tensor, parity_out: torch.Tensor, stream=None) -> None:
+    """parity_out[s, r] = parity_in[s, r] ^ E[k+r][target] * (old[s] ^ new[s]); in place allowed."""
+    B, L = old.shape
+    check(lib.elect_ec_encode_update_batch(coder.handle, L, B, target, _column(old), _column(new),
+                                           _shards(parity_in), _shards(parity_out), _stream(stream)),
+          "encode_update_batch")
+
+
+def apply_batch(coef: np.ndarray, src, dst, stream=None) -> None:
+    """dst[r] = XOR_j coef[r, j] * src[j] over [B, L] column tensors."""
+    coef = np.ascontiguousarray(coef, np.uint8)
+    rows, cols = coef.shape
+    B, L = src[0].shape
+    s = (ColumnT * cols)(*[_column(t) for t in src])
+    d = (ColumnT * rows)(*[_column(t) for t in dst])
+    check(lib.elect_ec_apply_batch(coef.ctypes.data_as(_lib._u8p), rows, cols, L, B, s, d, _stream(stream)),
+          "apply_batch")
+
+
+def partition_by_bytes(sizes, world: int, rank: int):
+    """Contiguous block of work items for `rank` so that every rank gets about
+    the same number of bytes (stripes are independent: no exchange step).
+    sizes: bytes per item, in order.  Returns (begin, end)."""
+    sizes = np.asarray(sizes, dtype=np.int64)
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    if sizes.size == 0:
+        return 0, 0
+    cum = np.concatenate([[0], np.cumsum(sizes)])
+    total = cum[-1]
+    bounds = [int(np.searchsorted(cum, total * r / world, side="left")) for r in range(world + 1)]
+    bounds[0], bounds[-1] = 0, sizes.size
+    for i in range(1, world + 1):
+        bounds[i] = max(bounds[i], bounds[i - 1])
+    return bounds[rank], bounds[rank + 1]

@@ -1,0 +1,494 @@
+// ec_capi.cpp — the C ABI (include/elect_ec.h) over the gfx950 kernels.
+//
+// EC/  = src/elect/src/native/src/org/apache/cassandra/io/erasurecode
+// JEC/ = src/elect/src/java/org/apache/cassandra/io/erasurecode
+//
+// Host work here is the reference's O(k^3) coder logic (matrix generation,
+// survivor-matrix inversion, decode-row selection); every byte of stripe data
+// goes through rs_kernels.hip.  There is no CPU fallback: without a device the
+// calls return ELECT_EC_ENODEV.
+#include "../../include/elect_ec.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <new>
+
+#include "gf256.hpp"
+#include "rs_kernels.hpp"
+
+struct elect_ec_coder {
+    int k = 0;
+    int m = 0;
+    // (k+m) x k generator, rows past k+m stay zero (as the zeroed MMAX x KMAX
+    // array of IsalEncoder/IsalDecoder, EC/erasure_coder.h:45-53).
+    uint8_t gen[ELECT_EC_MAX_UNITS * ELECT_EC_MAX_DATA_UNITS] = {};
+};
+
+namespace {
+
+using elect::kern::ApplyParams;
+using elect::kern::Column;
+using elect::kern::UpdateParams;
+
+int map_hip(hipError_t e)
+{
+    switch (e) {
+    case hipSuccess: return ELECT_EC_OK;
+    case hipErrorNoDevice:
+    case hipErrorInvalidDevice:
+    case hipErrorNoBinaryForGpu: return ELECT_EC_ENODEV;
+    case hipErrorOutOfMemory: return ELECT_EC_ENOMEM;
+    case hipErrorInvalidValue: return ELECT_EC_EINVAL;
+    default: return ELECT_EC_EDEVICE;
+    }
+}
+
+const uint8_t* parity_row(const elect_ec_coder* c, int r) { return c->gen + (c->k + r) * c->k; }
+
+// processErasures + generateDecodeMatrix (EC/erasure_coder.c:161-200, 241-284).
+// compat: rows r < numErasedDataUnits follow the reference's two loops, the
+// rest stay zero (clearDecoder, :229-238); strict: every row reconstructs its
+// unit.  A singular survivor set: strict -> ESINGULAR; compat -> the partially
+// reduced inverse is used, as the reference ignores gf_invert_matrix's -1
+// (:257-258), and WARN_SINGULAR is returned.
+int build_decode_matrix(const elect_ec_coder* c, const int* decode_indexes, const int* erased,
+                        int num_erased, int mode, uint8_t* out)
+{
+    const int k = c->k, n = c->k + c->m;
+    if (!decode_indexes || (num_erased > 0 && !erased) || !out) return ELECT_EC_EINVAL;
+    if (num_erased < 0 || num_erased > c->m) return ELECT_EC_EINVAL;  // JEC/CoderUtil.java:79-82
+    if (mode != ELECT_EC_DECODE_COMPAT && mode != ELECT_EC_DECODE_STRICT) return ELECT_EC_EINVAL;
+    for (int j = 0; j < k; ++j)
+        if (decode_indexes[j] < 0 || decode_indexes[j] >= n) return ELECT_EC_EINVAL;
+    for (int r = 0; r < num_erased; ++r)
+        if (erased[r] < 0 || erased[r] >= n) return ELECT_EC_EINVAL;
+
+    uint8_t work[ELECT_EC_MAX_DATA_UNITS * ELECT_EC_MAX_DATA_UNITS];
+    uint8_t inv[ELECT_EC_MAX_DATA_UNITS * ELECT_EC_MAX_DATA_UNITS];
+    for (int i = 0; i < k; ++i) std::memcpy(work + i * k, c->gen + decode_indexes[i] * k, k);
+    const bool ok = elect::gf::invert(work, inv, k);
+    if (!ok && mode == ELECT_EC_DECODE_STRICT) return ELECT_EC_ESINGULAR;
+
+    std::memset(out, 0, static_cast<size_t>(num_erased) * k);
+    int rows = num_erased;
+    if (mode == ELECT_EC_DECODE_COMPAT) {
+        rows = 0;  // numErasedDataUnits (EC/erasure_coder.c:177-182)
+        for (int r = 0; r < num_erased; ++r) rows += erased[r] < k;
+    }
+    for (int r = 0; r < rows; ++r) {
+        const int e = erased[r];
+        if (e < k) {
+            std::memcpy(out + r * k, inv + e * k, k);
+        } else {
+            const uint8_t* g = c->gen + e * k;  // parity unit: E[e] * Inv
+            for (int i = 0; i < k; ++i) {
+                uint8_t s = 0;
+                for (int j = 0; j < k; ++j) s ^= elect::gf::mul(inv[j * k + i], g[j]);
+                out[r * k + i] = s;
+            }
+        }
+    }
+    return ok ? ELECT_EC_OK : ELECT_EC_WARN_SINGULAR;
+}
+
+hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
+
+Column col(const void* base, size_t stripe_stride, size_t offset)
+{
+    Column c;
+    c.ptr = static_cast<const uint8_t*>(base) + offset;
+    c.stride = stripe_stride;
+    return c;
+}
+
+// ---------------------------------------------------------------------------
+// Host-memory path: per-thread, per-device staging engine.
+// Input chunks are copied into pinned buffers, sent H2D, coded, returned D2H
+// and copied out, with two slots (streams) so chunk c+1's transfers overlap
+// chunk c's kernel and host copies.
+// ---------------------------------------------------------------------------
+struct HostOp {
+    int cols = 0;
+    int rows = 0;
+    bool update = false;  // cols = 2 + rows: [old, new, P...]; else an apply
+    const unsigned char* const* in = nullptr;
+    unsigned char* const* out = nullptr;
+    uint8_t coef[elect::kern::kMaxRows * elect::kern::kMaxCols] = {};
+};
+
+class HostEngine {
+public:
+    static constexpr size_t kChunk = size_t{1} << 20;  // bytes per shard per pipeline step
+    static constexpr int kSlots = 2;
+
+    explicit HostEngine(int dev) : dev_(dev) {}
+    ~HostEngine()
+    {
+        for (int s = 0; s < kSlots; ++s) {
+            if (stream_[s]) (void)hipStreamDestroy(stream_[s]);
+            if (pin_in_[s]) (void)hipHostFree(pin_in_[s]);
+            if (pin_out_[s]) (void)hipHostFree(pin_out_[s]);
+            if (d_in_[s]) (void)hipFree(d_in_[s]);
+            if (d_out_[s]) (void)hipFree(d_out_[s]);
+        }
+    }
+
+    int run(const HostOp& op, size_t len)
+    {
+        const size_t step = std::min(len, kChunk);
+        const size_t pitch = (step + 255) & ~size_t{255};
+        int rc = reserve(static_cast<size_t>(op.cols) * pitch, static_cast<size_t>(op.rows) * pitch);
+        if (rc != ELECT_EC_OK) return rc;
+        const size_t nchunks = (len + step - 1) / step;
+        size_t pending[kSlots] = {};
+        bool busy[kSlots] = {};
+        for (size_t c = 0; c < nchunks + kSlots; ++c) {
+            const int s = static_cast<int>(c % kSlots);
+            if (busy[s]) {  // retire the chunk that used this slot
+                const hipError_t e = hipStreamSynchronize(stream_[s]);
+                if (e != hipSuccess) return map_hip(e);
+                const size_t o = pending[s] * step;
+                const size_t n = std::min(step, len - o);
+                for (int r = 0; r < op.rows; ++r) std::memcpy(op.out[r] + o, pin_out_[s] + r * pitch, n);
+                busy[s] = false;
+            }
+            if (c >= nchunks) continue;
+            const size_t o = c * step;
+            const size_t n = std::min(step, len - o);
+            for (int j = 0; j < op.cols; ++j) std::memcpy(pin_in_[s] + j * pitch, op.in[j] + o, n);
+            hipError_t e = hipMemcpyAsync(d_in_[s], pin_in_[s], op.cols * pitch, hipMemcpyHostToDevice, stream_[s]);
+            if (e == hipSuccess) e = launch(op, s, pitch, n);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(pin_out_[s], d_out_[s], op.rows * pitch, hipMemcpyDeviceToHost, stream_[s]);
+            if (e != hipSuccess) {
+                (void)hipStreamSynchronize(stream_[0]);
+                (void)hipStreamSynchronize(stream_[1]);
+                return map_hip(e);
+            }
+            pending[s] = c;
+            busy[s] = true;
+        }
+        return ELECT_EC_OK;
+    }
+
+private:
+    hipError_t launch(const HostOp& op, int s, size_t pitch, size_t n)
+    {
+        if (op.update) {
+            UpdateParams p;
+            p.len = n;
+            p.stripes = 1;
+            p.rows = op.rows;
+            p.old_data = col(d_in_[s], pitch, 0);
+            p.new_data = col(d_in_[s], pitch, pitch);
+            for (int r = 0; r < op.rows; ++r) {
+                p.par_in[r] = col(d_in_[s], pitch, (2 + r) * pitch);
+                p.par_out[r] = col(d_out_[s], pitch, r * pitch);
+                p.coef[r] = op.coef[r];
+            }
+            return elect::kern::launch_update(p, stream_[s]);
+        }
+        ApplyParams p;
+        p.len = n;
+        p.stripes = 1;
+        p.cols = op.cols;
+        p.rows = op.rows;
+        for (int j = 0; j < op.cols; ++j) p.src[j] = col(d_in_[s], pitch, j * pitch);
+        for (int r = 0; r < op.rows; ++r) p.dst[r] = col(d_out_[s], pitch, r * pitch);
+        std::memcpy(p.coef, op.coef, sizeof(p.coef));
+        return elect::kern::launch_apply(p, stream_[s]);
+    }
+
+    int reserve(size_t in_bytes, size_t out_bytes)
+    {
+        if (!stream_[0]) {
+            for (int s = 0; s < kSlots; ++s) {
+                const hipError_t e = hipStreamCreateWithFlags(&stream_[s], hipStreamNonBlocking);
+                if (e != hipSuccess) return map_hip(e);
+            }
+        }
+        if (in_bytes > cap_in_) {
+            for (int s = 0; s < kSlots; ++s) {
+                if (pin_in_[s]) (void)hipHostFree(pin_in_[s]);
+                if (d_in_[s]) (void)hipFree(d_in_[s]);
+                pin_in_[s] = nullptr;
+                d_in_[s] = nullptr;
+                hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&pin_in_[s]), in_bytes, hipHostMallocDefault);
+                if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_in_[s]), in_bytes);
+                if (e != hipSuccess) {
+                    cap_in_ = 0;
+                    return map_hip(e);
+                }
+            }
+            cap_in_ = in_bytes;
+        }
+        if (out_bytes > cap_out_) {
+            for (int s = 0; s < kSlots; ++s) {
+                if (pin_out_[s]) (void)hipHostFree(pin_out_[s]);
+                if (d_out_[s]) (void)hipFree(d_out_[s]);
+                pin_out_[s] = nullptr;
+                d_out_[s] = nullptr;
+                hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&pin_out_[s]), out_bytes, hipHostMallocDefault);
+                if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_out_[s]), out_bytes);
+                if (e != hipSuccess) {
+                    cap_out_ = 0;
+                    return map_hip(e);
+                }
+            }
+            cap_out_ = out_bytes;
+        }
+        return ELECT_EC_OK;
+    }
+
+    int dev_;
+    hipStream_t stream_[kSlots] = {};
+    uint8_t* pin_in_[kSlots] = {};
+    uint8_t* pin_out_[kSlots] = {};
+    uint8_t* d_in_[kSlots] = {};
+    uint8_t* d_out_[kSlots] = {};
+    size_t cap_in_ = 0;
+    size_t cap_out_ = 0;
+};
+
+constexpr int kMaxDevices = 64;
+thread_local std::unique_ptr<HostEngine> t_engines[kMaxDevices];
+
+int run_host(const HostOp& op, size_t len)
+{
+    if (len == 0) return ELECT_EC_OK;  // JEC/ErasureEncoder.java:41-44, JEC/ErasureDecoder.java:36-38
+    for (int j = 0; j < op.cols; ++j)
+        if (!op.in[j]) return ELECT_EC_EINVAL;
+    for (int r = 0; r < op.rows; ++r)
+        if (!op.out[r]) return ELECT_EC_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return ELECT_EC_ENODEV;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return map_hip(e);
+    if (dev < 0 || dev >= kMaxDevices) return ELECT_EC_ENODEV;
+    if (!t_engines[dev]) {
+        t_engines[dev].reset(new (std::nothrow) HostEngine(dev));
+        if (!t_engines[dev]) return ELECT_EC_ENOMEM;
+    }
+    return t_engines[dev]->run(op, len);
+}
+
+bool valid_coder(const elect_ec_coder* c) { return c && c->k >= 1 && c->m >= 1; }
+
+}  // namespace
+
+extern "C" {
+
+const char* elect_ec_version(void) { return "elect-ec-mi355x 0.1 (gfx950)"; }
+
+const char* elect_ec_strerror(int status)
+{
+    switch (status) {
+    case ELECT_EC_OK: return "ok";
+    case ELECT_EC_WARN_SINGULAR: return "decode ran on a singular survivor set (compat mode)";
+    case ELECT_EC_EINVAL: return "invalid argument";
+    case ELECT_EC_ESINGULAR: return "survivor matrix is singular";
+    case ELECT_EC_EDEVICE: return "HIP device error";
+    case ELECT_EC_ENOMEM: return "out of memory";
+    case ELECT_EC_ENODEV: return "no HIP device";
+    default: return "unknown status";
+    }
+}
+
+int elect_ec_device_count(int* count)
+{
+    if (!count) return ELECT_EC_EINVAL;
+    int n = 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    *count = e == hipSuccess ? n : 0;
+    return (e == hipSuccess && n > 0) ? ELECT_EC_OK : ELECT_EC_ENODEV;
+}
+
+int elect_ec_coder_create(int num_data_units, int num_parity_units, elect_ec_coder** out)
+{
+    if (!out) return ELECT_EC_EINVAL;
+    *out = nullptr;
+    const int k = num_data_units, m = num_parity_units;
+    if (k < 1 || m < 1 || k > ELECT_EC_MAX_DATA_UNITS || k + m > ELECT_EC_MAX_UNITS) return ELECT_EC_EINVAL;
+    auto* c = new (std::nothrow) elect_ec_coder;
+    if (!c) return ELECT_EC_ENOMEM;
+    c->k = k;
+    c->m = m;
+    elect::gf::cauchy_generator(k, m, c->gen);  // initEncodeMatrix, EC/erasure_coder.c:39-47
+    *out = c;
+    return ELECT_EC_OK;
+}
+
+void elect_ec_coder_destroy(elect_ec_coder* coder) { delete coder; }
+
+int elect_ec_coder_num_data_units(const elect_ec_coder* coder) { return coder ? coder->k : ELECT_EC_EINVAL; }
+
+int elect_ec_coder_num_parity_units(const elect_ec_coder* coder) { return coder ? coder->m : ELECT_EC_EINVAL; }
+
+int elect_ec_coder_encode_matrix(const elect_ec_coder* coder, unsigned char* out, size_t out_len)
+{
+    if (!valid_coder(coder) || !out) return ELECT_EC_EINVAL;
+    const size_t n = static_cast<size_t>(coder->k + coder->m) * coder->k;
+    if (out_len < n) return ELECT_EC_EINVAL;
+    std::memcpy(out, coder->gen, n);
+    return ELECT_EC_OK;
+}
+
+int elect_ec_coder_gf_tables(const elect_ec_coder* coder, unsigned char* out, size_t out_len)
+{
+    if (!valid_coder(coder) || !out) return ELECT_EC_EINVAL;
+    const size_t n = static_cast<size_t>(coder->m) * coder->k * 32;
+    if (out_len < n) return ELECT_EC_EINVAL;
+    elect::gf::isal_tables(parity_row(coder, 0), coder->m, coder->k, out);
+    return ELECT_EC_OK;
+}
+
+int elect_ec_coder_decode_matrix(const elect_ec_coder* coder, const int* decode_indexes,
+                                 const int* erased_indexes, int num_erased, int mode, unsigned char* out)
+{
+    if (!valid_coder(coder)) return ELECT_EC_EINVAL;
+    return build_decode_matrix(coder, decode_indexes, erased_indexes, num_erased, mode, out);
+}
+
+// ---- host memory ----
+
+int elect_ec_encode(const elect_ec_coder* coder, const unsigned char* const* data_units,
+                    unsigned char* const* parity_units, size_t chunk_size)
+{
+    if (!valid_coder(coder) || !data_units || !parity_units) return ELECT_EC_EINVAL;
+    HostOp op;
+    op.cols = coder->k;
+    op.rows = coder->m;
+    op.in = data_units;
+    op.out = parity_units;
+    for (int r = 0; r < coder->m; ++r) std::memcpy(op.coef + r * op.cols, parity_row(coder, r), coder->k);
+    return run_host(op, chunk_size);
+}
+
+int elect_ec_encode_update(const elect_ec_coder* coder, const unsigned char* const* old_new_parity,
+                           int target_data_index, unsigned char* const* new_parity_units, size_t chunk_size)
+{
+    if (!valid_coder(coder) || !old_new_parity || !new_parity_units) return ELECT_EC_EINVAL;
+    if (target_data_index < 0 || target_data_index >= coder->k) return ELECT_EC_EINVAL;
+    HostOp op;
+    op.update = true;
+    op.cols = 2 + coder->m;
+    op.rows = coder->m;
+    op.in = old_new_parity;
+    op.out = new_parity_units;
+    for (int r = 0; r < coder->m; ++r) op.coef[r] = parity_row(coder, r)[target_data_index];
+    return run_host(op, chunk_size);
+}
+
+int elect_ec_decode(const elect_ec_coder* coder, const unsigned char* const* inputs, const int* decode_indexes,
+                    const int* erased_indexes, int num_erased, unsigned char* const* outputs, size_t chunk_size,
+                    int mode)
+{
+    if (!valid_coder(coder) || !inputs || (num_erased > 0 && !outputs)) return ELECT_EC_EINVAL;
+    HostOp op;
+    const int st = build_decode_matrix(coder, decode_indexes, erased_indexes, num_erased, mode, op.coef);
+    if (st < 0) return st;
+    if (num_erased == 0) return st;
+    op.cols = coder->k;
+    op.rows = num_erased;
+    op.in = inputs;
+    op.out = outputs;
+    const int rc = run_host(op, chunk_size);
+    return rc != ELECT_EC_OK ? rc : st;
+}
+
+// ---- device resident ----
+
+int elect_ec_encode_batch(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                          elect_ec_shards data, elect_ec_shards parity, void* stream)
+{
+    if (!valid_coder(coder) || (!data.base && num_stripes && chunk_size) ||
+        (!parity.base && num_stripes && chunk_size))
+        return ELECT_EC_EINVAL;
+    ApplyParams p;
+    p.len = chunk_size;
+    p.stripes = num_stripes;
+    p.cols = coder->k;
+    p.rows = coder->m;
+    for (int j = 0; j < p.cols; ++j) p.src[j] = col(data.base, data.stripe_stride, j * data.shard_stride);
+    for (int r = 0; r < p.rows; ++r) {
+        p.dst[r] = col(parity.base, parity.stripe_stride, r * parity.shard_stride);
+        std::memcpy(p.coef + r * p.cols, parity_row(coder, r), coder->k);
+    }
+    return map_hip(elect::kern::launch_apply(p, as_stream(stream)));
+}
+
+int elect_ec_decode_batch(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                          elect_ec_shards inputs, const int* decode_indexes, const int* erased_indexes,
+                          int num_erased, elect_ec_shards outputs, unsigned flags, int mode, void* stream)
+{
+    if (!valid_coder(coder)) return ELECT_EC_EINVAL;
+    ApplyParams p;
+    const int st = build_decode_matrix(coder, decode_indexes, erased_indexes, num_erased, mode, p.coef);
+    if (st < 0) return st;
+    if (num_erased == 0 || chunk_size == 0 || num_stripes == 0) return st;
+    if (!inputs.base || !outputs.base) return ELECT_EC_EINVAL;
+    p.len = chunk_size;
+    p.stripes = num_stripes;
+    p.cols = coder->k;
+    p.rows = num_erased;
+    for (int j = 0; j < p.cols; ++j) {
+        const size_t slot = (flags & ELECT_EC_INPUTS_BY_UNIT) ? static_cast<size_t>(decode_indexes[j]) : j;
+        p.src[j] = col(inputs.base, inputs.stripe_stride, slot * inputs.shard_stride);
+    }
+    for (int r = 0; r < p.rows; ++r) {
+        const size_t slot = (flags & ELECT_EC_OUTPUTS_BY_UNIT) ? static_cast<size_t>(erased_indexes[r]) : r;
+        p.dst[r] = col(outputs.base, outputs.stripe_stride, slot * outputs.shard_stride);
+    }
+    const int rc = map_hip(elect::kern::launch_apply(p, as_stream(stream)));
+    return rc != ELECT_EC_OK ? rc : st;
+}
+
+int elect_ec_encode_update_batch(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                                 int target_data_index, elect_ec_column old_data, elect_ec_column new_data,
+                                 elect_ec_shards parity_in, elect_ec_shards parity_out, void* stream)
+{
+    if (!valid_coder(coder) || target_data_index < 0 || target_data_index >= coder->k) return ELECT_EC_EINVAL;
+    if (chunk_size == 0 || num_stripes == 0) return ELECT_EC_OK;
+    if (!old_data.ptr || !new_data.ptr || !parity_in.base || !parity_out.base) return ELECT_EC_EINVAL;
+    UpdateParams p;
+    p.len = chunk_size;
+    p.stripes = num_stripes;
+    p.rows = coder->m;
+    p.old_data = col(old_data.ptr, old_data.stripe_stride, 0);
+    p.new_data = col(new_data.ptr, new_data.stripe_stride, 0);
+    for (int r = 0; r < p.rows; ++r) {
+        p.par_in[r] = col(parity_in.base, parity_in.stripe_stride, r * parity_in.shard_stride);
+        p.par_out[r] = col(parity_out.base, parity_out.stripe_stride, r * parity_out.shard_stride);
+        p.coef[r] = parity_row(coder, r)[target_data_index];
+    }
+    return map_hip(elect::kern::launch_update(p, as_stream(stream)));
+}
+
+int elect_ec_apply_batch(const unsigned char* coef, int rows, int cols, size_t chunk_size, size_t num_stripes,
+                         const elect_ec_column* src, const elect_ec_column* dst, void* stream)
+{
+    if (!coef || !src || !dst || rows < 1 || cols < 1 || rows > ELECT_EC_MAX_APPLY || cols > ELECT_EC_MAX_APPLY)
+        return ELECT_EC_EINVAL;
+    ApplyParams p;
+    p.len = chunk_size;
+    p.stripes = num_stripes;
+    p.cols = cols;
+    p.rows = rows;
+    for (int j = 0; j < cols; ++j) {
+        if (!src[j].ptr && chunk_size && num_stripes) return ELECT_EC_EINVAL;
+        p.src[j] = col(src[j].ptr, src[j].stripe_stride, 0);
+    }
+    for (int r = 0; r < rows; ++r) {
+        if (!dst[r].ptr && chunk_size && num_stripes) return ELECT_EC_EINVAL;
+        p.dst[r] = col(dst[r].ptr, dst[r].stripe_stride, 0);
+    }
+    std::memcpy(p.coef, coef, static_cast<size_t>(rows) * cols);
+    return map_hip(elect::kern::launch_apply(p, as_stream(stream)));
+}
+
+}  // extern "C"

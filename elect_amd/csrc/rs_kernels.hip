@@ -1,0 +1,452 @@
+// rs_kernels.hip — gfx950 (MI355X, CDNA4) kernels for ELECT's Reed-Solomon path.
+//
+// The reference runs every encode/decode byte through ISA-L's ec_encode_data
+// (EC/erasure_coder.c:90 and :221) and every parity update through
+// ec_encode_data_update (EC/erasure_coder.c:128), one stripe per CPU thread.
+// Here a launch covers a whole batch of stripes.
+//
+// Work unit: a 16-byte segment of one stripe.  A lane loads the segment from
+// each source column (global_load_dwordx4, 1 KiB contiguous per wave
+// instruction), multiplies and XOR-accumulates it into every output row in
+// registers, and stores each row's 16 bytes (global_store_dwordx4).  Each input
+// byte is read once and each output byte written once, so the kernel streams
+// (cols + rows) x len bytes per stripe and is bound by HBM, not by ALU.
+//
+// GF(2^8) multiply by a wave-uniform coefficient c uses byte shuffles, not
+// MFMA: split x into bit fields x[2:0], x[5:3], x[7:6]; then
+//   c*x = T0[x[2:0]] ^ T1[x[5:3]] ^ T2[x[7:6]]
+// (GF multiplication is linear over GF(2)).  An 8-entry byte table is two
+// dwords, so ONE v_perm_b32 looks up four bytes at once; the tables stay in
+// SGPRs (kernel arguments, scalar loads), one table dword per v_perm moves to a
+// VGPR once per coefficient.  Per data dword: 5 VALU ops for the three bit-field
+// selectors (shared by all rows) + per row 3 v_perm + 1.5 XOR (v_bitop3 XOR3).
+//
+// Tails: ELECT's chunk length (ceil(sstable_size * 1.05), StorageService.java:
+// 331-339) is not a multiple of 16.  The dwordx4 kernels cover the whole
+// 16-byte segments of every stripe; the last len % 16 bytes per stripe go to a
+// second, byte-granular launch.  Layouts whose column starts are not all
+// 16-byte aligned run the byte-granular kernel for everything (any pointer).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <mutex>
+
+#include "rs_kernels.hpp"
+
+namespace elect {
+namespace kern {
+namespace {
+
+constexpr int kBlock = 256;
+
+// q = (n * m) >> p is exact floor(n / d) for every n < 2^31 (m = ceil(2^p/d),
+// p = 31 + ceil(log2 d); the rounding error m*d - 2^p < d keeps n*err < 2^p).
+struct Magic {
+    uint32_t m;
+    uint32_t p;
+};
+
+Magic make_magic(uint32_t d)
+{
+    uint32_t l = 0;
+    while ((uint64_t{1} << l) < d) ++l;
+    const uint32_t p = 31 + l;
+    const uint64_t m = ((uint64_t{1} << p) + d - 1) / d;
+    return Magic{static_cast<uint32_t>(m), p};
+}
+
+constexpr uint64_t kMaxIndex = (uint64_t{1} << 31) - 1;
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// One coefficient applied to four packed bytes, given the three selectors.
+__device__ __forceinline__ uint32_t gf_lookup(const gf::PermTable& t, uint32_t s0, uint32_t s1,
+                                              uint32_t s2)
+{
+    return xor3(__builtin_amdgcn_perm(t.t0_hi, t.t0_lo, s0),
+                __builtin_amdgcn_perm(t.t1_hi, t.t1_lo, s1), __builtin_amdgcn_perm(t.t2, t.t2, s2));
+}
+
+struct Sel {
+    uint32_t s0, s1, s2;
+};
+
+__device__ __forceinline__ Sel selectors(uint32_t x)
+{
+    return Sel{x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u};
+}
+
+__device__ __forceinline__ uint32_t lane_word(const uint4& v, int w)
+{
+    return w == 0 ? v.x : w == 1 ? v.y : w == 2 ? v.z : v.w;
+}
+
+__device__ __forceinline__ void set_word(uint4& v, int w, uint32_t x)
+{
+    if (w == 0) v.x = x;
+    else if (w == 1) v.y = x;
+    else if (w == 2) v.z = x;
+    else v.w = x;
+}
+
+// ---------------------------------------------------------------------------
+// Fast path: K source columns, R output rows, U segments per lane.
+// ---------------------------------------------------------------------------
+template <int K, int R>
+struct FastArgs {
+    const uint8_t* sp[K];
+    uint64_t ss[K];
+    uint8_t* dp[R];
+    uint64_t ds[R];
+    uint32_t segs;   // whole 16-byte segments per stripe
+    uint32_t total;  // segments in this launch (< 2^31)
+    uint32_t magic;
+    uint32_t shift;
+    gf::PermTable tab[R][K];
+};
+
+template <int K, int R, int U>
+__global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
+{
+    const uint32_t first = blockIdx.x * (kBlock * U) + threadIdx.x;
+    uint4 x[U][K];
+    uint32_t stripe[U];
+    uint64_t off[U];
+    bool live[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t idx = first + u * kBlock;
+        const uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
+        stripe[u] = s;
+        off[u] = static_cast<uint64_t>(idx - s * a.segs) * 16;
+        live[u] = idx < a.total;
+        if (live[u]) {
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                x[u][j] = *reinterpret_cast<const uint4*>(a.sp[j] + s * a.ss[j] + off[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (!live[u]) continue;
+        uint4 acc[R];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            uint32_t ar[R];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const Sel s = selectors(lane_word(x[u][j], w));
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t v = gf_lookup(a.tab[r][j], s.s0, s.s1, s.s2);
+                    ar[r] = j == 0 ? v : (ar[r] ^ v);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) set_word(acc[r], w, ar[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            *reinterpret_cast<uint4*>(a.dp[r] + stripe[u] * a.ds[r] + off[u]) = acc[r];
+    }
+}
+
+template <int K>
+constexpr int segs_per_lane()
+{
+    return K <= 4 ? 2 : 1;
+}
+
+template <int K, int R>
+hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
+{
+    constexpr int U = segs_per_lane<K>();
+    FastArgs<K, R> a{};
+    const uint64_t segs64 = p.len / 16;
+    if (segs64 == 0) return hipSuccess;
+    if (segs64 > kMaxIndex) return hipErrorInvalidValue;
+    a.segs = static_cast<uint32_t>(segs64);
+    const Magic mg = make_magic(a.segs);
+    a.magic = mg.m;
+    a.shift = mg.p;
+    for (int r = 0; r < R; ++r)
+        for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(p.coef[(r0 + r) * p.cols + j]);
+    const uint64_t per_launch = kMaxIndex / segs64;  // stripes per launch keeping idx < 2^31
+    for (uint64_t s0 = 0; s0 < p.stripes; s0 += per_launch) {
+        const uint64_t ns = std::min<uint64_t>(per_launch, p.stripes - s0);
+        for (int j = 0; j < K; ++j) {
+            a.sp[j] = p.src[j].ptr + s0 * p.src[j].stride;
+            a.ss[j] = p.src[j].stride;
+        }
+        for (int r = 0; r < R; ++r) {
+            a.dp[r] = const_cast<uint8_t*>(p.dst[r0 + r].ptr) + s0 * p.dst[r0 + r].stride;
+            a.ds[r] = p.dst[r0 + r].stride;
+        }
+        a.total = static_cast<uint32_t>(ns * segs64);
+        const uint32_t grid = (a.total + kBlock * U - 1) / (kBlock * U);
+        hipLaunchKernelGGL((gf_apply_x16<K, R, U>), dim3(grid), dim3(kBlock), 0, stream, a);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+using FastFn = hipError_t (*)(const ApplyParams&, int, hipStream_t);
+
+template <int K>
+constexpr std::array<FastFn, kFastRows> fast_row_fns()
+{
+    return {&launch_fast_kr<K, 1>, &launch_fast_kr<K, 2>, &launch_fast_kr<K, 3>, &launch_fast_kr<K, 4>};
+}
+
+const std::array<std::array<FastFn, kFastRows>, kMaxCols> kFast = {
+    fast_row_fns<1>(),  fast_row_fns<2>(),  fast_row_fns<3>(),  fast_row_fns<4>(),
+    fast_row_fns<5>(),  fast_row_fns<6>(),  fast_row_fns<7>(),  fast_row_fns<8>(),
+    fast_row_fns<9>(),  fast_row_fns<10>(), fast_row_fns<11>(), fast_row_fns<12>(),
+    fast_row_fns<13>(), fast_row_fns<14>(), fast_row_fns<15>(), fast_row_fns<16>()};
+
+// ---------------------------------------------------------------------------
+// Byte-granular path: any alignment, any (cols, rows) up to 16 x 16.
+// ---------------------------------------------------------------------------
+struct GenericArgs {
+    const uint8_t* sp[kMaxCols];
+    uint64_t ss[kMaxCols];
+    uint8_t* dp[kMaxRows];
+    uint64_t ds[kMaxRows];
+    uint32_t len;    // bytes per stripe in this launch window (< 2^31)
+    uint32_t total;  // bytes in this launch
+    uint32_t magic;
+    uint32_t shift;
+    int cols;
+    int rows;
+    uint8_t coef[kMaxRows * kMaxCols];
+};
+
+__constant__ uint8_t d_exp[512];
+__constant__ uint8_t d_log[256];
+
+__global__ __launch_bounds__(kBlock) void gf_apply_bytes(const GenericArgs a)
+{
+    const uint32_t idx = blockIdx.x * kBlock + threadIdx.x;
+    if (idx >= a.total) return;
+    const uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
+    const uint32_t i = idx - s * a.len;
+    uint8_t lx[kMaxCols];
+    bool nz[kMaxCols];
+    for (int j = 0; j < a.cols; ++j) {
+        const uint8_t v = a.sp[j][s * a.ss[j] + i];
+        nz[j] = v != 0;
+        lx[j] = d_log[v];
+    }
+    for (int r = 0; r < a.rows; ++r) {
+        uint8_t acc = 0;
+        for (int j = 0; j < a.cols; ++j) {
+            const uint8_t c = a.coef[r * a.cols + j];
+            if (c != 0 && nz[j]) acc ^= d_exp[d_log[c] + lx[j]];
+        }
+        a.dp[r][s * a.ds[r] + i] = acc;
+    }
+}
+
+hipError_t launch_bytes(const ApplyParams& p, hipStream_t stream)
+{
+    static std::mutex mu;             // field tables go to __constant__ once per device
+    static uint64_t ready_mask = 0;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        if (!(ready_mask & (uint64_t{1} << (dev & 63)))) {
+            e = hipMemcpyToSymbol(HIP_SYMBOL(d_exp), gf::kField.exp.data(), 512);
+            if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(d_log), gf::kField.log.data(), 256);
+            if (e != hipSuccess) return e;
+            ready_mask |= uint64_t{1} << (dev & 63);
+        }
+    }
+    if (p.len > kMaxIndex) return hipErrorInvalidValue;
+    GenericArgs a{};
+    a.len = static_cast<uint32_t>(p.len);
+    a.cols = p.cols;
+    a.rows = p.rows;
+    std::copy(p.coef, p.coef + kMaxRows * kMaxCols, a.coef);
+    const Magic mg = make_magic(a.len);
+    a.magic = mg.m;
+    a.shift = mg.p;
+    const uint64_t per_launch = kMaxIndex / p.len;
+    for (uint64_t s0 = 0; s0 < p.stripes; s0 += per_launch) {
+        const uint64_t ns = std::min<uint64_t>(per_launch, p.stripes - s0);
+        for (int j = 0; j < p.cols; ++j) {
+            a.sp[j] = p.src[j].ptr + s0 * p.src[j].stride;
+            a.ss[j] = p.src[j].stride;
+        }
+        for (int r = 0; r < p.rows; ++r) {
+            a.dp[r] = const_cast<uint8_t*>(p.dst[r].ptr) + s0 * p.dst[r].stride;
+            a.ds[r] = p.dst[r].stride;
+        }
+        a.total = static_cast<uint32_t>(ns * p.len);
+        const uint32_t grid = (a.total + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL(gf_apply_bytes, dim3(grid), dim3(kBlock), 0, stream, a);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------
+// Parity update: par_out[r] = par_in[r] ^ c_r * (old ^ new), fused.
+// ---------------------------------------------------------------------------
+template <int R>
+struct UpdArgs {
+    const uint8_t* op;
+    uint64_t os;
+    const uint8_t* np;
+    uint64_t ns;
+    const uint8_t* pip[R];
+    uint64_t pis[R];
+    uint8_t* pop[R];
+    uint64_t pos[R];
+    uint32_t segs, total, magic, shift;
+    gf::PermTable tab[R];
+};
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void gf_update_x16(const UpdArgs<R> a)
+{
+    const uint32_t idx = blockIdx.x * kBlock + threadIdx.x;
+    if (idx >= a.total) return;
+    const uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
+    const uint64_t b0 = static_cast<uint64_t>(idx - s * a.segs) * 16;
+    const uint4 o = *reinterpret_cast<const uint4*>(a.op + s * a.os + b0);
+    const uint4 w = *reinterpret_cast<const uint4*>(a.np + s * a.ns + b0);
+    uint4 pin[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) pin[r] = *reinterpret_cast<const uint4*>(a.pip[r] + s * a.pis[r] + b0);
+    const uint4 d = make_uint4(o.x ^ w.x, o.y ^ w.y, o.z ^ w.z, o.w ^ w.w);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const Sel sl = selectors(lane_word(d, q));
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            set_word(pin[r], q, lane_word(pin[r], q) ^ gf_lookup(a.tab[r], sl.s0, sl.s1, sl.s2));
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) *reinterpret_cast<uint4*>(a.pop[r] + s * a.pos[r] + b0) = pin[r];
+}
+
+template <int R>
+hipError_t launch_update_r(const UpdateParams& p, int r0, hipStream_t stream)
+{
+    UpdArgs<R> a{};
+    const uint64_t segs64 = p.len / 16;
+    if (segs64 == 0) return hipSuccess;
+    if (segs64 > kMaxIndex) return hipErrorInvalidValue;
+    a.segs = static_cast<uint32_t>(segs64);
+    const Magic mg = make_magic(a.segs);
+    a.magic = mg.m;
+    a.shift = mg.p;
+    for (int r = 0; r < R; ++r) a.tab[r] = gf::perm_table(p.coef[r0 + r]);
+    const uint64_t per_launch = kMaxIndex / segs64;
+    for (uint64_t s0 = 0; s0 < p.stripes; s0 += per_launch) {
+        const uint64_t ns = std::min<uint64_t>(per_launch, p.stripes - s0);
+        a.op = p.old_data.ptr + s0 * p.old_data.stride;
+        a.os = p.old_data.stride;
+        a.np = p.new_data.ptr + s0 * p.new_data.stride;
+        a.ns = p.new_data.stride;
+        for (int r = 0; r < R; ++r) {
+            a.pip[r] = p.par_in[r0 + r].ptr + s0 * p.par_in[r0 + r].stride;
+            a.pis[r] = p.par_in[r0 + r].stride;
+            a.pop[r] = const_cast<uint8_t*>(p.par_out[r0 + r].ptr) + s0 * p.par_out[r0 + r].stride;
+            a.pos[r] = p.par_out[r0 + r].stride;
+        }
+        a.total = static_cast<uint32_t>(ns * segs64);
+        const uint32_t grid = (a.total + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL((gf_update_x16<R>), dim3(grid), dim3(kBlock), 0, stream, a);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+using UpdFn = hipError_t (*)(const UpdateParams&, int, hipStream_t);
+const std::array<UpdFn, kFastRows> kUpd = {&launch_update_r<1>, &launch_update_r<2>,
+                                           &launch_update_r<3>, &launch_update_r<4>};
+
+bool col_aligned(const Column& c) { return ((reinterpret_cast<uintptr_t>(c.ptr) | c.stride) & 15u) == 0; }
+
+// The last len % 16 bytes of every stripe, as a byte-granular launch.
+ApplyParams tail_of(const ApplyParams& p)
+{
+    ApplyParams q = p;
+    const uint64_t body = p.len & ~uint64_t{15};
+    for (int j = 0; j < p.cols; ++j) q.src[j].ptr = p.src[j].ptr + body;
+    for (int r = 0; r < p.rows; ++r) q.dst[r].ptr = p.dst[r].ptr + body;
+    q.len = p.len - body;
+    return q;
+}
+
+// The update as a (2 + rows)-column product [c_r, c_r, e_r] over [old, new, P...].
+ApplyParams update_as_apply(const UpdateParams& p)
+{
+    ApplyParams q;
+    q.len = p.len;
+    q.stripes = p.stripes;
+    q.cols = 2 + p.rows;
+    q.rows = p.rows;
+    q.src[0] = p.old_data;
+    q.src[1] = p.new_data;
+    for (int r = 0; r < p.rows; ++r) {
+        q.src[2 + r] = p.par_in[r];
+        q.dst[r] = p.par_out[r];
+        q.coef[r * q.cols + 0] = p.coef[r];
+        q.coef[r * q.cols + 1] = p.coef[r];
+        q.coef[r * q.cols + 2 + r] = 1;
+    }
+    return q;
+}
+
+}  // namespace
+
+bool apply_is_aligned(const ApplyParams& p)
+{
+    for (int j = 0; j < p.cols; ++j)
+        if (!col_aligned(p.src[j])) return false;
+    for (int r = 0; r < p.rows; ++r)
+        if (!col_aligned(p.dst[r])) return false;
+    return true;
+}
+
+hipError_t launch_apply(const ApplyParams& p, hipStream_t stream)
+{
+    if (p.cols < 1 || p.cols > kMaxCols || p.rows < 1 || p.rows > kMaxRows) return hipErrorInvalidValue;
+    if (p.len == 0 || p.stripes == 0) return hipSuccess;
+    if (!apply_is_aligned(p)) return launch_bytes(p, stream);
+    for (int r0 = 0; r0 < p.rows; r0 += kFastRows) {
+        const int nr = std::min(kFastRows, p.rows - r0);
+        const hipError_t e = kFast[p.cols - 1][nr - 1](p, r0, stream);
+        if (e != hipSuccess) return e;
+    }
+    return (p.len & 15) ? launch_bytes(tail_of(p), stream) : hipSuccess;
+}
+
+hipError_t launch_update(const UpdateParams& p, hipStream_t stream)
+{
+    if (p.rows < 1 || p.rows > kMaxRows || p.rows + 2 > kMaxCols) return hipErrorInvalidValue;
+    if (p.len == 0 || p.stripes == 0) return hipSuccess;
+    bool aligned = col_aligned(p.old_data) && col_aligned(p.new_data);
+    for (int r = 0; r < p.rows; ++r) aligned = aligned && col_aligned(p.par_in[r]) && col_aligned(p.par_out[r]);
+    if (!aligned) return launch_bytes(update_as_apply(p), stream);
+    for (int r0 = 0; r0 < p.rows; r0 += kFastRows) {
+        const int nr = std::min(kFastRows, p.rows - r0);
+        const hipError_t e = kUpd[nr - 1](p, r0, stream);
+        if (e != hipSuccess) return e;
+    }
+    return (p.len & 15) ? launch_bytes(tail_of(update_as_apply(p)), stream) : hipSuccess;
+}
+
+}  // namespace kern
+}  // namespace elect

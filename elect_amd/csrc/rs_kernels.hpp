@@ -1,0 +1,62 @@
+// rs_kernels.hpp — internal launch interface of the gfx950 GF(2^8) kernels.
+//
+// One kernel family serves every byte-stream operation of ELECT's coder:
+//   encode        -> ec_encode_data(len, k, m, ...)          EC/erasure_coder.c:90
+//   decode        -> ec_encode_data(len, k, numErased, ...)  EC/erasure_coder.c:221
+//   encodeUpdate  -> ec_encode_data_update(...)              EC/erasure_coder.c:128
+// all as  dst[r][i] = XOR_j coef[r][j] * src[j][i]  over a batch of stripes.
+// (EC/ = src/elect/src/native/src/org/apache/cassandra/io/erasurecode)
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "gf256.hpp"
+
+namespace elect {
+namespace kern {
+
+constexpr int kMaxCols = 16;  // source columns per launch
+constexpr int kMaxRows = 16;  // output rows per call (fast kernels take 4 per launch)
+constexpr int kFastRows = 4;
+
+// A shard column over a batch of stripes: stripe s's bytes start at ptr + s*stride.
+struct Column {
+    const uint8_t* ptr = nullptr;
+    uint64_t stride = 0;
+};
+
+struct ApplyParams {
+    Column src[kMaxCols];
+    Column dst[kMaxRows];  // written through (uint8_t*)ptr
+    uint64_t len = 0;      // bytes per shard
+    uint64_t stripes = 0;  // stripes in the batch
+    int cols = 0;
+    int rows = 0;
+    uint8_t coef[kMaxRows * kMaxCols] = {};  // rows x cols, row-major
+};
+
+// par_out[r] = par_in[r] ^ coef[r] * (old ^ new): ec_encode_data_update with
+// ELECT's old^new folding (EC/erasure_coder.c:100-142), fused into one pass.
+struct UpdateParams {
+    Column old_data;
+    Column new_data;
+    Column par_in[kMaxRows];
+    Column par_out[kMaxRows];
+    uint64_t len = 0;
+    uint64_t stripes = 0;
+    int rows = 0;
+    uint8_t coef[kMaxRows] = {};
+};
+
+hipError_t launch_apply(const ApplyParams& p, hipStream_t stream);
+hipError_t launch_update(const UpdateParams& p, hipStream_t stream);
+
+// True when every column start is 16-byte aligned for every stripe, i.e. the
+// dwordx4 fast kernels apply; otherwise the byte-granular kernel runs.
+bool apply_is_aligned(const ApplyParams& p);
+
+}  // namespace kern
+}  // namespace elect

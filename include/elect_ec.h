@@ -1,0 +1,144 @@
+/*
+ * elect_ec.h — C ABI of the MI355X erasure-coding engine that replaces ELECT's
+ * JNI library libec.so (a thin ISA-L wrapper built by EC/genlib.sh:22-26).
+ *
+ * EC/  = src/elect/src/native/src/org/apache/cassandra/io/erasurecode
+ * JEC/ = src/elect/src/java/org/apache/cassandra/io/erasurecode
+ *
+ * Plain C types only (pointers, sizes, ints); no HIP or torch types appear in
+ * the signatures: a hip stream is passed as `void*` (hipStream_t), NULL = the
+ * default stream of the calling thread's current device.
+ *
+ * Threading: a coder is immutable after elect_ec_coder_create(), so every call
+ * below is re-entrant and may run concurrently on one coder or on many (the
+ * reference shares per-call scratch inside the coder, EC/NativeRSEncoder.c:25-29,
+ * EC/erasure_coder.h:50-65, and is safe only because ELECT makes a coder per
+ * task).  create/destroy must not race with other calls on the same coder,
+ * exactly as Java's write lock already ensures (JEC/NativeRSEncoder.java:33-92).
+ *
+ * Errors: every function returns an int status (ELECT_EC_OK = 0); nothing is
+ * thrown across the ABI.  The JNI shim maps them to the Java
+ * exceptions the reference raises (EC/jni_common.h:29-36).
+ */
+#ifndef ELECT_EC_H
+#define ELECT_EC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ELECT_EC_MAX_DATA_UNITS 10 /* KMAX, EC/erasure_coder.h:34 */
+#define ELECT_EC_MAX_UNITS 14      /* MMAX, EC/erasure_coder.h:33 */
+#define ELECT_EC_MAX_APPLY 16      /* rows / columns of elect_ec_apply_batch */
+
+/* status codes */
+#define ELECT_EC_OK 0
+#define ELECT_EC_WARN_SINGULAR 1 /* compat decode ran on a singular survivor set, as libec.so does */
+#define ELECT_EC_EINVAL (-1)     /* bad argument (counts, indexes, NULL pointers)           */
+#define ELECT_EC_ESINGULAR (-2)  /* strict decode: survivor rows are not invertible           */
+#define ELECT_EC_EDEVICE (-3)    /* HIP runtime error                                          */
+#define ELECT_EC_ENOMEM (-4)     /* host or device allocation failed                           */
+#define ELECT_EC_ENODEV (-5)     /* no usable MI355X device                                    */
+
+/* decode modes */
+#define ELECT_EC_DECODE_COMPAT 0 /* bit-exact libec.so: rows past the erased DATA count are zero
+                                    (EC/erasure_coder.c:261-281) */
+#define ELECT_EC_DECODE_STRICT 1 /* every erased unit (data or parity) reconstructed */
+
+/* decode_batch layout flags */
+#define ELECT_EC_INPUTS_BY_UNIT 1u  /* survivor j at inputs.base + decode_indexes[j]*shard_stride
+                                       (stripe-resident layout); default: j*shard_stride */
+#define ELECT_EC_OUTPUTS_BY_UNIT 2u /* output r at outputs.base + erased[r]*shard_stride
+                                       (rebuild in place); default: r*shard_stride */
+
+typedef struct elect_ec_coder elect_ec_coder;
+
+/* A set of shards over a batch of stripes on the device: shard i of stripe s
+ * starts at base + s*stripe_stride + i*shard_stride. */
+typedef struct elect_ec_shards {
+    void* base;
+    size_t stripe_stride;
+    size_t shard_stride;
+} elect_ec_shards;
+
+/* One column of an arbitrary product: stripe s at ptr + s*stripe_stride. */
+typedef struct elect_ec_column {
+    void* ptr;
+    size_t stripe_stride;
+} elect_ec_column;
+
+const char* elect_ec_version(void);
+const char* elect_ec_strerror(int status);
+/* Number of visible HIP devices (0 with ELECT_EC_ENODEV when none). */
+int elect_ec_device_count(int* count);
+
+/* ---- coder lifecycle ----
+ * Replaces initEncoder / initDecoder (EC/erasure_coder.c:49-72) as called by
+ * NativeRSEncoder_initImpl (EC/NativeRSEncoder.c:31-40) and NativeRSDecoder_initImpl
+ * (EC/NativeRSDecoder.c:32-41); destroy replaces the destroyImpl pair
+ * (EC/NativeRSEncoder.c:86-95, EC/NativeRSDecoder.c:73-82).  Host-only work.
+ * Limits as the reference: 1 <= k <= 10, m >= 1, k + m <= 14. */
+int elect_ec_coder_create(int num_data_units, int num_parity_units, elect_ec_coder** out);
+void elect_ec_coder_destroy(elect_ec_coder* coder);
+int elect_ec_coder_num_data_units(const elect_ec_coder* coder);
+int elect_ec_coder_num_parity_units(const elect_ec_coder* coder);
+/* (k+m) x k generator (gf_gen_cauchy1_matrix, EC/erasure_coder.c:43). */
+int elect_ec_coder_encode_matrix(const elect_ec_coder* coder, unsigned char* out, size_t out_len);
+/* m*k*32 bytes of ISA-L-layout tables for the parity rows (ec_init_tables,
+ * EC/erasure_coder.c:57-59) — for callers that persist or compare them. */
+int elect_ec_coder_gf_tables(const elect_ec_coder* coder, unsigned char* out, size_t out_len);
+/* num_erased x k decode matrix exactly as processErasures/generateDecodeMatrix
+ * build it (EC/erasure_coder.c:161-200, 241-284) in the given mode.  Returns
+ * ELECT_EC_WARN_SINGULAR (compat) or ELECT_EC_ESINGULAR (strict) for a singular
+ * survivor set. */
+int elect_ec_coder_decode_matrix(const elect_ec_coder* coder, const int* decode_indexes,
+                                 const int* erased_indexes, int num_erased, int mode,
+                                 unsigned char* out);
+
+/* ---- host memory, synchronous: the JNI calling convention ----
+ * Replace encode / encodeUpdate / decode (EC/erasure_coder.h:77-79, bodies at
+ * EC/erasure_coder.c:74-98, 100-142, 202-226).  Buffers are host pointers
+ * (JVM direct ByteBuffers + position, EC/jni_common.c:62-108); outputs are
+ * complete when the call returns.  Runs on the calling thread's current HIP
+ * device through per-thread pinned staging and two streams. */
+int elect_ec_encode(const elect_ec_coder* coder, const unsigned char* const* data_units,
+                    unsigned char* const* parity_units, size_t chunk_size);
+/* inputs: [old data, new data, old parity 0..m-1] (EC/NativeRSEncoder.c:79);
+ * outputs: m new parity units; may alias the old parity inputs. */
+int elect_ec_encode_update(const elect_ec_coder* coder, const unsigned char* const* old_new_parity,
+                           int target_data_index, unsigned char* const* new_parity_units,
+                           size_t chunk_size);
+/* inputs: k survivors ordered like decode_indexes[0..k-1]; outputs: num_erased. */
+int elect_ec_decode(const elect_ec_coder* coder, const unsigned char* const* inputs,
+                    const int* decode_indexes, const int* erased_indexes, int num_erased,
+                    unsigned char* const* outputs, size_t chunk_size, int mode);
+
+/* ---- device resident, batched, stream ordered ----
+ * Many stripes per launch.  All pointers are device pointers on the calling
+ * thread's current device; the call only enqueues work on `stream`.  16-byte
+ * aligned bases and strides take the dwordx4 kernels; anything else is still
+ * correct (byte-granular kernel). */
+int elect_ec_encode_batch(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                          elect_ec_shards data, elect_ec_shards parity, void* stream);
+int elect_ec_decode_batch(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                          elect_ec_shards inputs, const int* decode_indexes,
+                          const int* erased_indexes, int num_erased, elect_ec_shards outputs,
+                          unsigned flags, int mode, void* stream);
+/* parity_out[r] = parity_in[r] ^ E[k+r][target] * (old ^ new) for each stripe. */
+int elect_ec_encode_update_batch(const elect_ec_coder* coder, size_t chunk_size,
+                                 size_t num_stripes, int target_data_index,
+                                 elect_ec_column old_data, elect_ec_column new_data,
+                                 elect_ec_shards parity_in, elect_ec_shards parity_out,
+                                 void* stream);
+/* General product dst[r] = XOR_j coef[r*cols+j] * src[j], rows, cols <= 16. */
+int elect_ec_apply_batch(const unsigned char* coef, int rows, int cols, size_t chunk_size,
+                         size_t num_stripes, const elect_ec_column* src,
+                         const elect_ec_column* dst, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ELECT_EC_H */

@@ -1,0 +1,37 @@
+#!/bin/bash
+# GPU-box runner: each GPU step under its own time limit; stop on any fault,
+# abort, segfault, timeout or hang (exit codes other than 0 / pytest's 1).
+# usage: tools/gpu_run.sh step [step ...]   steps: smoke tests bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+TAG=${TAG:-r01}
+run() {  # name seconds cmd...
+    local name=$1 t=$2; shift 2
+    echo "[$(date +%T)] start $name" | tee -a gpurun_out/status.txt
+    timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "[$(date +%T)] $name rc=$rc" | tee -a gpurun_out/status.txt
+    tail -5 "gpurun_out/$name.log"
+    return $rc
+}
+for step in "$@"; do
+    case $step in
+    smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    tests)
+        run pytest_gpu 1000 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+        rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
+    bench) run bench 600 python bench.py || exit $? ;;
+    prof)
+        (cd /tmp && export TMPDIR=/tmp)
+        run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run \
+            -- python3 bench.py --no-cpu --no-host --steps 50 --warmup 5 || exit $? ;;
+    pmc)
+        run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_$TAG -o run \
+            -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $?
+        run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_$TAG -o run \
+            -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $? ;;
+    *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
