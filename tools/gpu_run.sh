@@ -6,6 +6,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
+export TMPDIR=/tmp
+OUT="$PWD/gpurun_out"
 TAG=${TAG:-r01}
 run() {  # name seconds cmd...
     local name=$1 t=$2; shift 2
@@ -24,13 +26,12 @@ for step in "$@"; do
         rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     bench) run bench 600 python bench.py || exit $? ;;
     prof)
-        (cd /tmp && export TMPDIR=/tmp)
-        run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run \
+        run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run \
             -- python3 bench.py --no-cpu --no-host --steps 50 --warmup 5 || exit $? ;;
     pmc)
-        run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_$TAG -o run \
+        run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_$TAG -o run \
             -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $?
-        run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_$TAG -o run \
+        run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run \
             -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
