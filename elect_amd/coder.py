@@ -47,6 +47,11 @@ class InternalError(RuntimeError):
     pass
 
 
+class NullPointerException(RuntimeError):
+    """java.lang.NullPointerException where the Java code dereferences a null
+    buffer before its own null check (JEC/ByteBufferDecodingState.java:56-59)."""
+
+
 # ---------------------------------------------------------------------------
 # java.nio.ByteBuffer subset
 # ---------------------------------------------------------------------------
@@ -310,6 +315,8 @@ class ByteBufferDecodingState:
         self.decodeLength = valid.remaining()
         self.usingDirectBuffer = valid.isDirect()
         self.inputOffsets = [b.position() if b is not None else 0 for b in inputs]
+        if any(b is None for b in outputs):
+            raise NullPointerException("outputs[i].position()")
         self.outputOffsets = [b.position() for b in outputs]
         CoderUtil.checkDecodeParameters(inputs, self.erasedIndexes, outputs,
                                         decoder.getNumDataUnits(), decoder.getNumParityUnits())

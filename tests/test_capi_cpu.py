@@ -1,0 +1,159 @@
+"""CPU: the C ABI library loads, exports every symbol include/elect_ec.h
+declares, and its host-side coder logic (generator matrix, ISA-L table layout,
+decode-matrix construction incl. ELECT's compat quirk and singular handling)
+matches the oracle and the golden fixtures.  No compute call needs a GPU here;
+the one that runs checks that the product fails loudly without one."""
+import ctypes
+import itertools
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT, gpu_available
+
+HEADER = os.path.join(ROOT, "include", "elect_ec.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(elect_ec_\w+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    from elect_amd import _lib
+    declared = header_functions()
+    assert len(declared) >= 17
+    for name in declared:
+        assert hasattr(_lib.lib, name), f"{name} missing from libelect_ec.so"
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    assert bound == set(declared), "ctypes bindings out of sync with the header"
+
+
+def test_library_links_hip_and_has_gfx950_code():
+    import subprocess
+    lib = os.path.join(ROOT, "elect_amd", "libelect_ec.so")
+    deps = subprocess.run(["ldd", lib], capture_output=True, text=True).stdout
+    assert "amdhip64" in deps
+    blob = open(lib, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_version_and_strerror():
+    from elect_amd import _lib
+    assert b"gfx950" in _lib.lib.elect_ec_version()
+    for st in (0, 1, -1, -2, -3, -4, -5):
+        assert _lib.strerror(st) != "unknown status"
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (8, 4), (1, 1), (10, 4), (2, 12), (3, 2)])
+def test_encode_matrix_and_tables_match_oracle(oracle, k, m):
+    from elect_amd.coder import RSCoder
+    c = RSCoder(k, m)
+    assert np.array_equal(c.encode_matrix(), oracle.cauchy_matrix(k, m))
+    assert np.array_equal(c.gf_tables(), oracle.init_tables(oracle.cauchy_matrix(k, m)[k:]))
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (3, 2), (8, 4), (6, 3)])
+def test_decode_matrix_all_patterns_match_oracle(oracle, k, m):
+    from elect_amd.coder import RSCoder
+    c = RSCoder(k, m)
+    rng = np.random.default_rng(k + m)
+    pats = [list(e) for n in range(1, m + 1) for e in itertools.combinations(range(k + m), n)]
+    for erased in pats:
+        surv = [i for i in range(k + m) if i not in erased][:k]
+        for order in (surv, [int(x) for x in rng.permutation(surv)]):
+            for mode in (0, 1):
+                st, mat = c.decode_matrix(order, erased, mode)
+                rc, want = oracle.decode_matrix(k, m, order, erased, bool(mode))
+                assert st == rc == 0
+                assert np.array_equal(mat, want), (erased, order, mode)
+
+
+def test_decode_matrix_golden():
+    from elect_amd.coder import RSCoder
+    from elect_amd import _lib
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "decode.json")))
+    coders = {}
+    for case in g["cases"]:
+        key = (case["k"], case["m"])
+        c = coders.setdefault(key, RSCoder(*key))
+        mode = _lib.DECODE_STRICT if case["mode"] == "strict" else _lib.DECODE_COMPAT
+        if case["status"] != 0 and mode == _lib.DECODE_STRICT:
+            with pytest.raises(_lib.ECSingularError):
+                c.decode_matrix(case["decode_indexes"], case["erased"], mode)
+            continue
+        st, mat = c.decode_matrix(case["decode_indexes"], case["erased"], mode)
+        expect_st = _lib.WARN_SINGULAR if case["status"] != 0 else _lib.OK
+        assert st == expect_st
+        assert mat.tobytes().hex() == case["matrix"], case
+
+
+def test_singular_compat_reproduces_partial_inverse(oracle):
+    """A duplicated survivor makes the k x k matrix singular; libec.so ignores
+    gf_invert_matrix's failure (EC/erasure_coder.c:257) and keeps going."""
+    from elect_amd.coder import RSCoder
+    from elect_amd import _lib
+    c = RSCoder(4, 2)
+    for surv in ([1, 1, 2, 3], [4, 4, 5, 0], [0, 1, 2, 2]):
+        for erased in ([0], [3], [0, 5], [5, 0]):
+            st, mat = c.decode_matrix(surv, erased, _lib.DECODE_COMPAT)
+            rc, want = oracle.decode_matrix(4, 2, surv, erased, False)
+            assert st == _lib.WARN_SINGULAR and rc == -1
+            assert np.array_equal(mat, want)
+
+
+def test_invalid_arguments():
+    from elect_amd import _lib
+    from elect_amd.coder import RSCoder
+    for k, m in ((0, 2), (11, 2), (4, 0), (10, 5), (-1, 1)):
+        with pytest.raises(_lib.ECInvalidArgument):
+            RSCoder(k, m)
+    c = RSCoder(4, 2)
+    with pytest.raises(_lib.ECInvalidArgument):
+        c.decode_matrix([1, 2, 3, 4], [0, 5, 1], 0)  # more erasures than m (JEC/CoderUtil.java:79-82)
+    with pytest.raises(_lib.ECInvalidArgument):
+        c.decode_matrix([1, 2, 3, 6], [0], 0)  # unit index out of range
+    with pytest.raises(_lib.ECInvalidArgument):
+        c.decode_matrix([1, 2, 3, 4], [0], 7)  # bad mode
+    h = ctypes.c_void_p()
+    assert _lib.lib.elect_ec_coder_create(4, 2, None) == _lib.EINVAL
+    assert _lib.lib.elect_ec_coder_create(4, 2, ctypes.byref(h)) == _lib.OK
+    assert _lib.lib.elect_ec_coder_num_data_units(h) == 4
+    assert _lib.lib.elect_ec_coder_num_parity_units(h) == 2
+    buf = (ctypes.c_ubyte * 8)()
+    assert _lib.lib.elect_ec_coder_encode_matrix(h, buf, 8) == _lib.EINVAL  # too small
+    _lib.lib.elect_ec_coder_destroy(h)
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks the no-device path")
+def test_no_device_fails_loudly():
+    """There is no CPU fallback: without a GPU, compute calls return ENODEV."""
+    from elect_amd import _lib
+    from elect_amd.coder import RSCoder
+    assert _lib.device_count() == 0
+    c = RSCoder(4, 2)
+    d = [np.zeros(64, np.uint8) for _ in range(4)]
+    p = [np.zeros(64, np.uint8) for _ in range(2)]
+    with pytest.raises(_lib.ECDeviceError):
+        c.encode_host([a.ctypes.data for a in d], [a.ctypes.data for a in p], 64)
+    # zero-length is a no-op before any device work (JEC/ErasureEncoder.java:41-44)
+    assert c.encode_host([a.ctypes.data for a in d], [a.ctypes.data for a in p], 0) == 0
+
+
+def test_partition_by_bytes():
+    from elect_amd.batch import partition_by_bytes
+    sizes = [1024] * 1000 + [4096] * 250 + [1 << 20] * 1
+    for world in (1, 2, 3, 4, 8):
+        parts = [partition_by_bytes(sizes, world, r) for r in range(world)]
+        assert parts[0][0] == 0 and parts[-1][1] == len(sizes)
+        for a, b in zip(parts, parts[1:]):
+            assert a[1] == b[0]
+    sizes = [65536] * 4096
+    for world in (1, 2, 4, 8):
+        for r in range(world):
+            b, e = partition_by_bytes(sizes, world, r)
+            assert e - b == 4096 // world
