@@ -211,7 +211,7 @@ def main():
     dec_alg = B * (k + 1) * L         # (k+e)*L per stripe, e = 1
     enc_gbs = enc_alg / (enc_ms * 1e-3) / 1e9
     dec_gbs = dec_alg / (dec_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic("gf_apply_x16ILi4ELi2E")
+    traffic, traffic_src = pmc_traffic("gf_apply_x16<4, 2")
 
     out = {
         "metric": "GiB/s device-resident RS(6,4) encode+decode, 64 KiB chunks, 1/2/4/8 GPU",

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Build the drop-in libec.so (JNI shim + MI355X engine) for ELECT.
+# Needs a JDK (for <jni.h>) and ROCm hipcc.  Not built in the CI image, which
+# has no JDK.  Usage: JAVA_HOME=/path/to/jdk elect_amd/csrc/jni/build_libec.sh [out_dir]
+set -euo pipefail
+HERE=$(cd "$(dirname "$0")" && pwd)
+ROOT=$(cd "$HERE/../../.." && pwd)
+OUT=${1:-$ROOT/build/libec}
+: "${JAVA_HOME:=$(dirname "$(dirname "$(readlink -f "$(which javac)")")")}"
+[ -f "$JAVA_HOME/include/jni.h" ] || { echo "no jni.h under JAVA_HOME=$JAVA_HOME" >&2; exit 1; }
+mkdir -p "$OUT"
+HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
+gcc -O2 -fPIC -Wall -c -I"$JAVA_HOME/include" -I"$JAVA_HOME/include/linux" -I"$ROOT/include" \
+    "$HERE/libec_jni.c" -o "$OUT/libec_jni.o"
+"$HIPCC" --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/include" -x hip -c \
+    "$ROOT/elect_amd/csrc/ec_capi.cpp" -o "$OUT/ec_capi.o"
+"$HIPCC" --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/include" -x hip -c \
+    "$ROOT/elect_amd/csrc/rs_kernels.hip" -o "$OUT/rs_kernels.o"
+"$HIPCC" --offload-arch=gfx950 -shared -fPIC -o "$OUT/libec.so" \
+    "$OUT/libec_jni.o" "$OUT/ec_capi.o" "$OUT/rs_kernels.o"
+echo "built $OUT/libec.so — copy it to \$CASSANDRA_HOME/lib/sigar-bin (README.md:60)"

@@ -1,0 +1,245 @@
+/*
+ * libec_jni.c — drop-in replacement for ELECT's JNI library libec.so.
+ *
+ * Exports exactly the seven native methods ELECT's Java binds
+ * (JEC/NativeRSEncoder.java:97-105, JEC/NativeRSDecoder.java:81-87; the
+ * reference implementations are EC/NativeRSEncoder.c:31-95 and
+ * EC/NativeRSDecoder.c:32-82) and forwards them to the MI355X C ABI
+ * (include/elect_ec.h).  Built only where a JDK provides <jni.h>; see
+ * INTEGRATION.md for the build line.  No Java code changes: ELECT keeps calling
+ * System.loadLibrary("ec") (JEC/NativeRSEncoder.java:37).
+ *
+ * Differences from the reference glue, all on error paths:
+ *  - every THROW returns (EC/NativeRSDecoder.c:50-52 and EC/jni_common.c:70-73,
+ *    95-97 fall through after throwing);
+ *  - int arrays are released (EC/jni_common.c:75, 99 and EC/NativeRSDecoder.c:59-62 leak);
+ *  - a negative engine status becomes a Java exception instead of being ignored;
+ *  - the three unconditional printf lines of decodeImpl (EC/NativeRSDecoder.c:57,
+ *    65, 68) print only when allowVerboseDump() is true.
+ *
+ * JEC/ = src/elect/src/java/org/apache/cassandra/io/erasurecode
+ * EC/  = src/elect/src/native/src/org/apache/cassandra/io/erasurecode
+ */
+#include <jni.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../../include/elect_ec.h"
+
+#define EC_MAX ELECT_EC_MAX_UNITS
+
+static void throw_java(JNIEnv* env, const char* cls, const char* msg)
+{
+    jclass c = (*env)->FindClass(env, cls);
+    if (c != NULL)
+        (*env)->ThrowNew(env, c, msg);
+}
+
+/* Map a C ABI status to the exception Java callers already handle. */
+static int raise_status(JNIEnv* env, int status, const char* what)
+{
+    char msg[160];
+    if (status >= 0)
+        return 0;
+    snprintf(msg, sizeof msg, "%s: %s (%d)", what, elect_ec_strerror(status), status);
+    if (status == ELECT_EC_EINVAL || status == ELECT_EC_ESINGULAR)
+        throw_java(env, "java/lang/IllegalArgumentException", msg);
+    else
+        throw_java(env, "java/io/IOException", msg);
+    return 1;
+}
+
+static jfieldID coder_field(JNIEnv* env, jobject thiz)
+{
+    jclass clazz = (*env)->GetObjectClass(env, thiz);
+    jfieldID fid = (*env)->GetFieldID(env, clazz, "nativeCoder", "J");
+    if (fid == NULL)
+        throw_java(env, "java/lang/UnsatisfiedLinkError", "Field nativeCoder not found");
+    return fid;
+}
+
+static int verbose(JNIEnv* env, jobject thiz)
+{
+    jclass clazz = (*env)->GetObjectClass(env, thiz);
+    jmethodID mid = (*env)->GetMethodID(env, clazz, "allowVerboseDump", "()Z");
+    if (mid == NULL) {
+        (*env)->ExceptionClear(env);
+        return 0;
+    }
+    return (*env)->CallBooleanMethod(env, thiz, mid) == JNI_TRUE;
+}
+
+/* getCoder, EC/jni_common.c:35-60 */
+static elect_ec_coder* get_coder(JNIEnv* env, jobject thiz)
+{
+    jfieldID fid = coder_field(env, thiz);
+    if (fid == NULL)
+        return NULL;
+    return (elect_ec_coder*)(intptr_t)(*env)->GetLongField(env, thiz, fid);
+}
+
+/* setCoder, EC/jni_common.c:24-33 */
+static void set_coder(JNIEnv* env, jobject thiz, elect_ec_coder* c)
+{
+    jfieldID fid = coder_field(env, thiz);
+    if (fid != NULL)
+        (*env)->SetLongField(env, thiz, fid, (jlong)(intptr_t)c);
+}
+
+/* getInputs/getOutputs, EC/jni_common.c:62-108: count check, then direct
+ * buffer address + offset per element.  Returns 0 on success. */
+static int buffers(JNIEnv* env, jobjectArray arr, jintArray offsets, int num, unsigned char** out,
+                   const char* what)
+{
+    if ((*env)->GetArrayLength(env, arr) != num || num > 2 + EC_MAX) {
+        throw_java(env, "java/lang/InternalError", what);
+        return 1;
+    }
+    jint* offs = (*env)->GetIntArrayElements(env, offsets, NULL);
+    if (offs == NULL)
+        return 1;
+    for (int i = 0; i < num; i++) {
+        jobject bb = (*env)->GetObjectArrayElement(env, arr, i);
+        unsigned char* base = bb ? (unsigned char*)(*env)->GetDirectBufferAddress(env, bb) : NULL;
+        out[i] = base ? base + offs[i] : NULL;
+        if (bb)
+            (*env)->DeleteLocalRef(env, bb);
+        if (out[i] == NULL) {
+            (*env)->ReleaseIntArrayElements(env, offsets, offs, JNI_ABORT);
+            throw_java(env, "java/lang/InternalError", what);
+            return 1;
+        }
+    }
+    (*env)->ReleaseIntArrayElements(env, offsets, offs, JNI_ABORT);
+    return 0;
+}
+
+JNIEXPORT void JNICALL
+Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_initImpl(JNIEnv* env, jobject thiz,
+                                                                  jint numDataUnits, jint numParityUnits)
+{
+    elect_ec_coder* c = NULL;
+    if (raise_status(env, elect_ec_coder_create(numDataUnits, numParityUnits, &c), "initImpl"))
+        return;
+    set_coder(env, thiz, c);
+}
+
+JNIEXPORT void JNICALL
+Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeImpl(JNIEnv* env, jobject thiz,
+                                                                    jobjectArray inputs, jintArray inputOffsets,
+                                                                    jint dataLen, jobjectArray outputs,
+                                                                    jintArray outputOffsets)
+{
+    unsigned char* in[2 + EC_MAX];
+    unsigned char* out[2 + EC_MAX];
+    elect_ec_coder* c = get_coder(env, thiz);
+    if (c == NULL) {
+        throw_java(env, "java/io/IOException", "NativeRSRawEncoder closed");
+        return;
+    }
+    int k = elect_ec_coder_num_data_units(c), m = elect_ec_coder_num_parity_units(c);
+    if (buffers(env, inputs, inputOffsets, k, in, "Invalid inputs") ||
+        buffers(env, outputs, outputOffsets, m, out, "Invalid outputs"))
+        return;
+    raise_status(env, elect_ec_encode(c, (const unsigned char* const*)in, out, (size_t)dataLen), "encode");
+}
+
+JNIEXPORT void JNICALL
+Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeUpdateImpl(JNIEnv* env, jobject thiz,
+                                                                          jobjectArray inputs,
+                                                                          jintArray inputOffsets, jint dataLen,
+                                                                          jint targetUpdateDataIndex,
+                                                                          jobjectArray outputs,
+                                                                          jintArray outputOffsets)
+{
+    unsigned char* in[2 + EC_MAX];
+    unsigned char* out[2 + EC_MAX];
+    elect_ec_coder* c = get_coder(env, thiz);
+    if (c == NULL) {
+        throw_java(env, "java/io/IOException", "NativeRSRawEncoder closed");
+        return;
+    }
+    int m = elect_ec_coder_num_parity_units(c);
+    if (buffers(env, inputs, inputOffsets, 2 + m, in, "Invalid inputs") ||
+        buffers(env, outputs, outputOffsets, m, out, "Invalid outputs"))
+        return;
+    raise_status(env,
+                 elect_ec_encode_update(c, (const unsigned char* const*)in, targetUpdateDataIndex, out,
+                                        (size_t)dataLen),
+                 "encodeUpdate");
+}
+
+JNIEXPORT void JNICALL
+Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_destroyImpl(JNIEnv* env, jobject thiz)
+{
+    elect_ec_coder* c = get_coder(env, thiz);
+    if (c != NULL) {
+        elect_ec_coder_destroy(c);
+        set_coder(env, thiz, NULL);
+    }
+}
+
+JNIEXPORT void JNICALL
+Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_initImpl(JNIEnv* env, jobject thiz,
+                                                                  jint numDataUnits, jint numParityUnits)
+{
+    elect_ec_coder* c = NULL;
+    if (raise_status(env, elect_ec_coder_create(numDataUnits, numParityUnits, &c), "initImpl"))
+        return;
+    set_coder(env, thiz, c);
+}
+
+/* ELECT_EC_DECODE_MODE=strict switches off the compat zero rows for every
+ * decoder in the process; the default is bit-exact libec.so. */
+static int decode_mode(void)
+{
+    const char* s = getenv("ELECT_EC_DECODE_MODE");
+    return (s != NULL && strcmp(s, "strict") == 0) ? ELECT_EC_DECODE_STRICT : ELECT_EC_DECODE_COMPAT;
+}
+
+JNIEXPORT void JNICALL
+Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_decodeImpl(JNIEnv* env, jobject thiz,
+                                                                    jobjectArray inputs, jintArray inputOffsets,
+                                                                    jint dataLen, jintArray decodeIndexes,
+                                                                    jintArray erasedIndexes, jobjectArray outputs,
+                                                                    jintArray outputOffsets)
+{
+    unsigned char* in[2 + EC_MAX];
+    unsigned char* out[2 + EC_MAX];
+    int dec[EC_MAX], era[EC_MAX];
+    elect_ec_coder* c = get_coder(env, thiz);
+    if (c == NULL) {
+        throw_java(env, "java/io/IOException", "NativeRSRawDecoder closed");
+        return;
+    }
+    int k = elect_ec_coder_num_data_units(c);
+    int n_dec = (*env)->GetArrayLength(env, decodeIndexes);
+    int n_era = (*env)->GetArrayLength(env, erasedIndexes);
+    if (n_dec < k || n_era > EC_MAX) {
+        throw_java(env, "java/lang/InternalError", "Invalid decode/erased indexes");
+        return;
+    }
+    (*env)->GetIntArrayRegion(env, decodeIndexes, 0, k, (jint*)dec);
+    (*env)->GetIntArrayRegion(env, erasedIndexes, 0, n_era, (jint*)era);
+    if (verbose(env, thiz))
+        printf("NativeRSDecoder_decodeImpl: k=%d erased=%d first=%d len=%d\n", k, n_era,
+               n_era > 0 ? era[0] : -1, (int)dataLen);
+    if (buffers(env, inputs, inputOffsets, k, in, "Invalid inputs") ||
+        buffers(env, outputs, outputOffsets, n_era, out, "Invalid outputs"))
+        return;
+    raise_status(env,
+                 elect_ec_decode(c, (const unsigned char* const*)in, dec, era, n_era, out, (size_t)dataLen,
+                                 decode_mode()),
+                 "decode");
+}
+
+JNIEXPORT void JNICALL
+Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_destroyImpl(JNIEnv* env, jobject thiz)
+{
+    elect_ec_coder* c = get_coder(env, thiz);
+    if (c != NULL) {
+        elect_ec_coder_destroy(c);
+        set_coder(env, thiz, NULL);
+    }
+}

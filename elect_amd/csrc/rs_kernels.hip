@@ -16,10 +16,10 @@
 // MFMA: split x into bit fields x[2:0], x[5:3], x[7:6]; then
 //   c*x = T0[x[2:0]] ^ T1[x[5:3]] ^ T2[x[7:6]]
 // (GF multiplication is linear over GF(2)).  An 8-entry byte table is two
-// dwords, so ONE v_perm_b32 looks up four bytes at once; the tables stay in
-// SGPRs (kernel arguments, scalar loads), one table dword per v_perm moves to a
-// VGPR once per coefficient.  Per data dword: 5 VALU ops for the three bit-field
-// selectors (shared by all rows) + per row 3 v_perm + 1.5 XOR (v_bitop3 XOR3).
+// dwords, so ONE v_perm_b32 looks up four bytes at once.  The tables are
+// staged in LDS per workgroup and read with wave-uniform (broadcast) ds_reads.
+// Per data dword: 5 VALU ops for the three bit-field selectors (shared by all
+// rows) + per row 3 v_perm + 2 XOR (one v_bitop3 XOR3).
 //
 // Tails: ELECT's chunk length (ceil(sstable_size * 1.05), StorageService.java:
 // 331-339) is not a multiple of 16.  The dwordx4 kernels cover the whole
@@ -93,8 +93,30 @@ __device__ __forceinline__ void set_word(uint4& v, int w, uint32_t x)
     else v.w = x;
 }
 
+// Streaming loads/stores: every byte is touched once, so keep it out of the
+// caches' way (global_load/store ... nt).  Measured on MI355X with
+// tools/tune/tune_apply.hip: +6-10 % over plain loads/stores on every BASELINE
+// shape ("Kernel tuning").
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 load_nt(const uint8_t* p)
+{
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ void store_nt(uint8_t* p, const uint4& v)
+{
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+}
+
 // ---------------------------------------------------------------------------
-// Fast path: K source columns, R output rows, U segments per lane.
+// Fast path: K source columns, R output rows, one 16-byte segment per lane.
+// The byte-shuffle tables (5 dwords per coefficient) are staged in LDS, padded
+// to 8 dwords so one ds_read_b128 + one ds_read_b32 (wave-uniform address,
+// broadcast) bring a coefficient's tables into VGPRs; keeping 32 coefficients
+// (RS(12,8)) in SGPRs instead spills.
 // ---------------------------------------------------------------------------
 template <int K, int R>
 struct FastArgs {
@@ -109,62 +131,65 @@ struct FastArgs {
     gf::PermTable tab[R][K];
 };
 
-template <int K, int R, int U>
+constexpr int kTabStride = 8;  // dwords per coefficient in LDS
+
+template <int K, int R>
 __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 {
-    const uint32_t first = blockIdx.x * (kBlock * U) + threadIdx.x;
-    uint4 x[U][K];
-    uint32_t stripe[U];
-    uint64_t off[U];
-    bool live[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint32_t idx = first + u * kBlock;
-        const uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
-        stripe[u] = s;
-        off[u] = static_cast<uint64_t>(idx - s * a.segs) * 16;
-        live[u] = idx < a.total;
-        if (live[u]) {
-#pragma unroll
-            for (int j = 0; j < K; ++j)
-                x[u][j] = *reinterpret_cast<const uint4*>(a.sp[j] + s * a.ss[j] + off[u]);
-        }
+    __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
+    for (int i = threadIdx.x; i < R * K; i += blockDim.x) {
+        const gf::PermTable& t = a.tab[i / K][i % K];
+        tl[i * kTabStride + 0] = t.t0_lo;
+        tl[i * kTabStride + 1] = t.t0_hi;
+        tl[i * kTabStride + 2] = t.t1_lo;
+        tl[i * kTabStride + 3] = t.t1_hi;
+        tl[i * kTabStride + 4] = t.t2;
     }
+    __syncthreads();
+
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.total) return;
+    const uint32_t stripe = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
+    const uint64_t off = static_cast<uint64_t>(idx - stripe * a.segs) * 16;
+
+    uint4 x[K];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        if (!live[u]) continue;
-        uint4 acc[R];
+    for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + stripe * a.ss[j] + off);
+
+    uint4 acc[R];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {  // column-outer: selectors once, then every row
+        uint32_t s0[4], s1[4], s2[4];
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-            uint32_t ar[R];
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                const Sel s = selectors(lane_word(x[u][j], w));
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const uint32_t v = gf_lookup(a.tab[r][j], s.s0, s.s1, s.s2);
-                    ar[r] = j == 0 ? v : (ar[r] ^ v);
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < R; ++r) set_word(acc[r], w, ar[r]);
+            const Sel sl = selectors(lane_word(x[j], w));
+            s0[w] = sl.s0;
+            s1[w] = sl.s1;
+            s2[w] = sl.s2;
         }
 #pragma unroll
-        for (int r = 0; r < R; ++r)
-            *reinterpret_cast<uint4*>(a.dp[r] + stripe[u] * a.ds[r] + off[u]) = acc[r];
+        for (int r = 0; r < R; ++r) {
+            const uint4 tq = *reinterpret_cast<const uint4*>(&tl[(r * K + j) * kTabStride]);
+            const uint32_t t2 = tl[(r * K + j) * kTabStride + 4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t v = xor3(__builtin_amdgcn_perm(tq.y, tq.x, s0[w]),
+                                        __builtin_amdgcn_perm(tq.w, tq.z, s1[w]),
+                                        __builtin_amdgcn_perm(t2, t2, s2[w]));
+                set_word(acc[r], w, j == 0 ? v : (lane_word(acc[r], w) ^ v));
+            }
+        }
     }
+#pragma unroll
+    for (int r = 0; r < R; ++r) store_nt(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
 }
 
-template <int K>
-constexpr int segs_per_lane()
-{
-    return K <= 4 ? 2 : 1;
-}
+// Small chunks (<= 4 KiB per shard) ran 3-4 % faster with 128-thread blocks.
+inline int block_for(uint64_t len) { return len <= 4096 ? 128 : kBlock; }
 
 template <int K, int R>
 hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
 {
-    constexpr int U = segs_per_lane<K>();
     FastArgs<K, R> a{};
     const uint64_t segs64 = p.len / 16;
     if (segs64 == 0) return hipSuccess;
@@ -175,6 +200,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     a.shift = mg.p;
     for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(p.coef[(r0 + r) * p.cols + j]);
+    const int block = block_for(p.len);
     const uint64_t per_launch = kMaxIndex / segs64;  // stripes per launch keeping idx < 2^31
     for (uint64_t s0 = 0; s0 < p.stripes; s0 += per_launch) {
         const uint64_t ns = std::min<uint64_t>(per_launch, p.stripes - s0);
@@ -187,8 +213,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             a.ds[r] = p.dst[r0 + r].stride;
         }
         a.total = static_cast<uint32_t>(ns * segs64);
-        const uint32_t grid = (a.total + kBlock * U - 1) / (kBlock * U);
-        hipLaunchKernelGGL((gf_apply_x16<K, R, U>), dim3(grid), dim3(kBlock), 0, stream, a);
+        const uint32_t grid = (a.total + block - 1) / block;
+        hipLaunchKernelGGL((gf_apply_x16<K, R>), dim3(grid), dim3(block), 0, stream, a);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -321,11 +347,11 @@ __global__ __launch_bounds__(kBlock) void gf_update_x16(const UpdArgs<R> a)
     if (idx >= a.total) return;
     const uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
     const uint64_t b0 = static_cast<uint64_t>(idx - s * a.segs) * 16;
-    const uint4 o = *reinterpret_cast<const uint4*>(a.op + s * a.os + b0);
-    const uint4 w = *reinterpret_cast<const uint4*>(a.np + s * a.ns + b0);
+    const uint4 o = load_nt(a.op + s * a.os + b0);
+    const uint4 w = load_nt(a.np + s * a.ns + b0);
     uint4 pin[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) pin[r] = *reinterpret_cast<const uint4*>(a.pip[r] + s * a.pis[r] + b0);
+    for (int r = 0; r < R; ++r) pin[r] = load_nt(a.pip[r] + s * a.pis[r] + b0);
     const uint4 d = make_uint4(o.x ^ w.x, o.y ^ w.y, o.z ^ w.z, o.w ^ w.w);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -335,7 +361,7 @@ __global__ __launch_bounds__(kBlock) void gf_update_x16(const UpdArgs<R> a)
             set_word(pin[r], q, lane_word(pin[r], q) ^ gf_lookup(a.tab[r], sl.s0, sl.s1, sl.s2));
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r) *reinterpret_cast<uint4*>(a.pop[r] + s * a.pos[r] + b0) = pin[r];
+    for (int r = 0; r < R; ++r) store_nt(a.pop[r] + s * a.pos[r] + b0, pin[r]);
 }
 
 template <int R>

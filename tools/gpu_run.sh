@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box runner: each GPU step under its own time limit; stop on any fault,
 # abort, segfault, timeout or hang (exit codes other than 0 / pytest's 1).
-# usage: tools/gpu_run.sh step [step ...]   steps: smoke tests bench prof pmc
+# usage: tools/gpu_run.sh step [step ...]   steps: smoke tests bench prof pmc tune
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -33,6 +33,7 @@ for step in "$@"; do
             -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $?
         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run \
             -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $? ;;
+    tune) run tune 600 tools/tune/tune_apply || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

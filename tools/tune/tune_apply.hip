@@ -1,0 +1,422 @@
+// tune_apply.hip — standalone variant sweep for the GF(2^8) batch kernel
+// (dev tooling, not product).  Times kernel variants on the BASELINE shapes in
+// ONE process with hipEvents (interleaved rounds, median), checks each against
+// the reference variant byte for byte, and reports GB/s of algorithmic traffic
+// ((cols + rows) * L per stripe) against the 8 TB/s HBM peak.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune/tune_apply.hip -o tune_apply
+//   ./tune_apply
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../elect_amd/csrc/gf256.hpp"
+
+#define CK(x)                                                                                   \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess) {                                                                 \
+            std::fprintf(stderr, "%s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            std::exit(3);                                                                       \
+        }                                                                                       \
+    } while (0)
+
+using elect::gf::PermTable;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 nt_load(const uint4* p)
+{
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nt_store(const uint4& v, uint4* p)
+{
+    u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+}
+
+template <int K, int R>
+struct Args {
+    const uint8_t* sp[K];
+    uint64_t ss[K];
+    uint8_t* dp[R];
+    uint64_t ds[R];
+    uint32_t segs, total, magic, shift;
+    PermTable tab[R][K];
+};
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t lane_word(const uint4& v, int w)
+{
+    return w == 0 ? v.x : w == 1 ? v.y : w == 2 ? v.z : v.w;
+}
+__device__ __forceinline__ void set_word(uint4& v, int w, uint32_t x)
+{
+    if (w == 0) v.x = x;
+    else if (w == 1) v.y = x;
+    else if (w == 2) v.z = x;
+    else v.w = x;
+}
+
+enum Mode { kGF = 0, kXor = 1 };
+enum Load { kPlain = 0, kNTL = 1, kNTS = 2, kNT = 3 };
+
+template <int K, int R, int U, int BLOCK, int MODE, int LD, bool GRIDSTRIDE, int ORDER = 0>
+__global__ __launch_bounds__(BLOCK) void kern(const Args<K, R> a)
+{
+    // ORDER 2: column-outer with the byte-shuffle tables staged in LDS
+    // (8 dwords per coefficient: t0_lo t0_hi t1_lo t1_hi t2 pad pad pad)
+    __shared__ __attribute__((aligned(16))) uint32_t tl[ORDER == 2 ? R * K * 8 : 4];
+    if (ORDER == 2) {
+        for (int i = threadIdx.x; i < R * K; i += BLOCK) {
+            const PermTable& t = a.tab[i / K][i % K];
+            tl[i * 8 + 0] = t.t0_lo; tl[i * 8 + 1] = t.t0_hi; tl[i * 8 + 2] = t.t1_lo;
+            tl[i * 8 + 3] = t.t1_hi; tl[i * 8 + 4] = t.t2;
+        }
+        __syncthreads();
+    }
+    const uint32_t step = GRIDSTRIDE ? gridDim.x * (BLOCK * U) : 0;
+    for (uint32_t first = blockIdx.x * (BLOCK * U) + threadIdx.x; first < a.total;
+         first += GRIDSTRIDE ? step : a.total) {
+        uint4 x[U][K];
+        uint32_t stripe[U];
+        uint64_t off[U];
+        bool live[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t idx = first + u * BLOCK;
+            const uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
+            stripe[u] = s;
+            off[u] = static_cast<uint64_t>(idx - s * a.segs) * 16;
+            live[u] = idx < a.total;
+            if (live[u]) {
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const uint4* p = reinterpret_cast<const uint4*>(a.sp[j] + s * a.ss[j] + off[u]);
+                    x[u][j] = (LD & kNTL) ? nt_load(p) : *p;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!live[u]) continue;
+            uint4 acc[R];
+            if (ORDER == 2 && MODE == kGF) {
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    uint32_t s0[4], s1[4], s2[4];
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const uint32_t v0 = lane_word(x[u][j], w);
+                        s0[w] = v0 & 0x07070707u;
+                        s1[w] = (v0 >> 3) & 0x07070707u;
+                        s2[w] = (v0 >> 6) & 0x03030303u;
+                    }
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const uint4 tq = *reinterpret_cast<const uint4*>(&tl[(r * K + j) * 8]);
+                        const uint32_t t2 = tl[(r * K + j) * 8 + 4];
+#pragma unroll
+                        for (int w = 0; w < 4; ++w) {
+                            const uint32_t v = xor3(__builtin_amdgcn_perm(tq.y, tq.x, s0[w]),
+                                                    __builtin_amdgcn_perm(tq.w, tq.z, s1[w]),
+                                                    __builtin_amdgcn_perm(t2, t2, s2[w]));
+                            set_word(acc[r], w, j == 0 ? v : (lane_word(acc[r], w) ^ v));
+                        }
+                    }
+                }
+            } else if (ORDER == 1 && MODE == kGF) {
+                // column-outer: selectors of one column, then every row, then every dword
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    uint32_t s0[4], s1[4], s2[4];
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const uint32_t v0 = lane_word(x[u][j], w);
+                        s0[w] = v0 & 0x07070707u;
+                        s1[w] = (v0 >> 3) & 0x07070707u;
+                        s2[w] = (v0 >> 6) & 0x03030303u;
+                    }
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const PermTable& t = a.tab[r][j];
+#pragma unroll
+                        for (int w = 0; w < 4; ++w) {
+                            const uint32_t v = xor3(__builtin_amdgcn_perm(t.t0_hi, t.t0_lo, s0[w]),
+                                                    __builtin_amdgcn_perm(t.t1_hi, t.t1_lo, s1[w]),
+                                                    __builtin_amdgcn_perm(t.t2, t.t2, s2[w]));
+                            set_word(acc[r], w, j == 0 ? v : (lane_word(acc[r], w) ^ v));
+                        }
+                    }
+                }
+            } else
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                uint32_t ar[R];
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const uint32_t v0 = lane_word(x[u][j], w);
+                    if (MODE == kXor) {
+#pragma unroll
+                        for (int r = 0; r < R; ++r) ar[r] = j == 0 ? v0 + r : (ar[r] ^ v0);
+                    } else {
+                        const uint32_t s0 = v0 & 0x07070707u, s1 = (v0 >> 3) & 0x07070707u,
+                                       s2 = (v0 >> 6) & 0x03030303u;
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const PermTable& t = a.tab[r][j];
+                            const uint32_t v = xor3(__builtin_amdgcn_perm(t.t0_hi, t.t0_lo, s0),
+                                                    __builtin_amdgcn_perm(t.t1_hi, t.t1_lo, s1),
+                                                    __builtin_amdgcn_perm(t.t2, t.t2, s2));
+                            ar[r] = j == 0 ? v : (ar[r] ^ v);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r) set_word(acc[r], w, ar[r]);
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                uint4* p = reinterpret_cast<uint4*>(a.dp[r] + stripe[u] * a.ds[r] + off[u]);
+                if (LD & kNTS) nt_store(acc[r], p);
+                else *p = acc[r];
+            }
+        }
+        if (!GRIDSTRIDE) break;
+    }
+}
+
+struct Magic {
+    uint32_t m, p;
+};
+static Magic make_magic(uint32_t d)
+{
+    uint32_t l = 0;
+    while ((uint64_t{1} << l) < d) ++l;
+    const uint32_t p = 31 + l;
+    return Magic{static_cast<uint32_t>(((uint64_t{1} << p) + d - 1) / d), p};
+}
+
+struct Shape {
+    const char* name;
+    int K, R;
+    uint64_t L, B;
+    int n_units;  // stripe row count (layout [B][n_units][L])
+};
+
+template <int K, int R>
+struct Runner {
+    Shape sh;
+    uint8_t* buf = nullptr;
+    uint8_t* out_ref = nullptr;
+    Args<K, R> a{};
+    int dev_cus = 256;
+
+    void setup(const Shape& s)
+    {
+        sh = s;
+        const uint64_t bytes = s.B * s.n_units * s.L;
+        CK(hipMalloc(&buf, bytes));
+        CK(hipMalloc(&out_ref, s.B * R * s.L));
+        // fill data with a device-side pattern via host staging (random)
+        std::vector<uint8_t> h(s.n_units * s.L);
+        uint64_t x = 0x243F6A8885A308D3ull;
+        for (uint64_t st = 0; st < s.B; st += 64) {
+            for (auto& c : h) {
+                x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+                c = static_cast<uint8_t>(x);
+            }
+            for (uint64_t t = st; t < std::min(s.B, st + 64); ++t)
+                CK(hipMemcpy(buf + t * s.n_units * s.L, h.data(), h.size(), hipMemcpyHostToDevice));
+        }
+        const uint64_t segs = s.L / 16;
+        a.segs = static_cast<uint32_t>(segs);
+        a.total = static_cast<uint32_t>(segs * s.B);
+        Magic mg = make_magic(a.segs);
+        a.magic = mg.m;
+        a.shift = mg.p;
+        uint8_t gen[14 * 10];
+        elect::gf::cauchy_generator(K, R, gen);
+        for (int j = 0; j < K; ++j) {
+            a.sp[j] = buf + j * s.L;
+            a.ss[j] = s.n_units * s.L;
+        }
+        for (int r = 0; r < R; ++r) {
+            a.dp[r] = buf + (K + r) * s.L;
+            a.ds[r] = s.n_units * s.L;
+            for (int j = 0; j < K; ++j) a.tab[r][j] = elect::gf::perm_table(gen[(K + r) * K + j]);
+        }
+        hipDeviceProp_t prop;
+        CK(hipGetDeviceProperties(&prop, 0));
+        dev_cus = prop.multiProcessorCount;
+    }
+
+    template <int U, int BLOCK, int MODE, int LD, bool GS, int ORDER = 0>
+    float time_one(int occ_blocks_per_cu, int iters)
+    {
+        const uint32_t per_block = BLOCK * U;
+        uint32_t grid = (a.total + per_block - 1) / per_block;
+        if (GS) grid = std::min<uint32_t>(grid, dev_cus * occ_blocks_per_cu);
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        std::vector<float> ts;
+        for (int i = 0; i < iters; ++i) {
+            CK(hipEventRecord(e0));
+            hipLaunchKernelGGL((kern<K, R, U, BLOCK, MODE, LD, GS, ORDER>), dim3(grid), dim3(BLOCK), 0, 0, a);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ts.push_back(ms);
+        }
+        CK(hipGetLastError());
+        std::sort(ts.begin(), ts.end());
+        CK(hipEventDestroy(e0));
+        CK(hipEventDestroy(e1));
+        return ts[ts.size() / 2];
+    }
+
+    // copy parity region to out_ref (reference output), compare
+    void snapshot()
+    {
+        for (int r = 0; r < R; ++r)
+            CK(hipMemcpy2D(out_ref + r * sh.L, R * sh.L, buf + (K + r) * sh.L, sh.n_units * sh.L, sh.L, sh.B,
+                           hipMemcpyDeviceToDevice));
+    }
+    bool same()
+    {
+        std::vector<uint8_t> a1(sh.L), b1(sh.L);
+        for (uint64_t st = 0; st < sh.B; st += std::max<uint64_t>(1, sh.B / 97)) {
+            for (int r = 0; r < R; ++r) {
+                CK(hipMemcpy(a1.data(), out_ref + (st * R + r) * sh.L, sh.L, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(b1.data(), buf + (st * sh.n_units + K + r) * sh.L, sh.L, hipMemcpyDeviceToHost));
+                if (std::memcmp(a1.data(), b1.data(), sh.L) != 0) return false;
+            }
+        }
+        return true;
+    }
+    void teardown()
+    {
+        CK(hipFree(buf));
+        CK(hipFree(out_ref));
+    }
+};
+
+static double alg_bytes(const Shape& s) { return double(s.B) * (s.K + s.R) * s.L; }
+
+template <int K, int R>
+static void sweep(const Shape& s)
+{
+    Runner<K, R> rn;
+    rn.setup(s);
+    const int it = 25;
+    // reference: U=2, 256, GF, plain
+    rn.template time_one<2, 256, kGF, kPlain, false>(0, 3);
+    rn.snapshot();
+    struct Row {
+        std::string name;
+        float ms;
+        bool ok;
+        bool check;
+    };
+    std::vector<Row> rows;
+    auto rec = [&](const char* n, float ms, bool check) { rows.push_back({n, ms, check ? rn.same() : true, check}); };
+    for (int round = 0; round < 3; ++round) {
+        rows.clear();
+        rec("U1 ntboth roworder", rn.template time_one<1, 256, kGF, kNT, false, 0>(0, it), true);
+        rec("U1 ntload roworder", rn.template time_one<1, 256, kGF, kNTL, false, 0>(0, it), true);
+        rec("U1 plain roworder", rn.template time_one<1, 256, kGF, kPlain, false, 0>(0, it), true);
+        rec("U1 ntboth colorder", rn.template time_one<1, 256, kGF, kNT, false, 1>(0, it), true);
+        rec("U1 ntload colorder", rn.template time_one<1, 256, kGF, kNTL, false, 1>(0, it), true);
+        rec("U1 ntboth LDS-tab", rn.template time_one<1, 256, kGF, kNT, false, 2>(0, it), true);
+        rec("U1 ntload LDS-tab", rn.template time_one<1, 256, kGF, kNTL, false, 2>(0, it), true);
+        rec("U1 plain LDS-tab", rn.template time_one<1, 256, kGF, kPlain, false, 2>(0, it), true);
+        rec("U1 ntstore LDS-tab", rn.template time_one<1, 256, kGF, kNTS, false, 2>(0, it), true);
+        rec("U1 b128 ntboth LDS-tab", rn.template time_one<1, 128, kGF, kNT, false, 2>(0, it), true);
+        rec("U1 b128 ntboth colorder", rn.template time_one<1, 128, kGF, kNT, false, 1>(0, it), true);
+        rec("U1 b128 ntload colorder", rn.template time_one<1, 128, kGF, kNTL, false, 1>(0, it), true);
+        rec("U1 XOR-only ntload", rn.template time_one<1, 256, kXor, kNTL, false>(0, it), false);
+        rec("U1 XOR-only nt both", rn.template time_one<1, 256, kXor, kNT, false>(0, it), false);
+        // restore reference output for later variants' checks
+        rn.template time_one<2, 256, kGF, kPlain, false>(0, 1);
+    }
+    std::printf("\n== %s: K=%d R=%d L=%llu B=%llu  alg %.3f GB/launch ==\n", s.name, K, R,
+                (unsigned long long)s.L, (unsigned long long)s.B, alg_bytes(s) / 1e9);
+    for (auto& r : rows)
+        std::printf("  %-30s %8.4f ms  %7.1f GB/s  %5.1f%% of 8 TB/s  %s\n", r.name.c_str(), r.ms,
+                    alg_bytes(s) / (r.ms * 1e-3) / 1e9, 100.0 * alg_bytes(s) / (r.ms * 1e-3) / 8e12,
+                    r.check ? (r.ok ? "bit-exact" : "MISMATCH") : "-");
+    rn.teardown();
+}
+
+__global__ void copy_kernel(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n)
+{
+    const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+    if (i < n) out[i] = in[i];
+}
+
+int main()
+{
+    int ndev = 0;
+    CK(hipGetDeviceCount(&ndev));
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    std::printf("device: %s  CUs=%d\n", prop.gcnArchName, prop.multiProcessorCount);
+    {  // plain copy reference: 1 GiB -> 1 GiB
+        const uint64_t bytes = 1ull << 30;
+        uint8_t *a, *b;
+        CK(hipMalloc(&a, bytes));
+        CK(hipMalloc(&b, bytes));
+        CK(hipMemset(a, 1, bytes));
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        std::vector<float> ts;
+        const uint64_t n = bytes / 16;
+        for (int i = 0; i < 25; ++i) {
+            CK(hipEventRecord(e0));
+            hipLaunchKernelGGL(copy_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, (const uint4*)a, (uint4*)b, n);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        std::printf("float4 copy 1 GiB: %.4f ms  %.1f GB/s (read+write) = %.1f%% of 8 TB/s\n", ts[12],
+                    2.0 * bytes / (ts[12] * 1e-3) / 1e9, 100.0 * 2.0 * bytes / (ts[12] * 1e-3) / 8e12);
+        ts.clear();
+        for (int i = 0; i < 25; ++i) {
+            CK(hipEventRecord(e0));
+            CK(hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, 0));
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        std::printf("hipMemcpy D2D 1 GiB: %.4f ms  %.1f GB/s (read+write)\n", ts[12],
+                    2.0 * bytes / (ts[12] * 1e-3) / 1e9);
+        CK(hipFree(a));
+        CK(hipFree(b));
+    }
+    sweep<4, 2>(Shape{"RS(6,4) encode 64KiB", 4, 2, 65536, 4096, 6});
+    sweep<4, 1>(Shape{"RS(6,4) decode e=1 64KiB", 4, 1, 65536, 4096, 6});
+    sweep<8, 2>(Shape{"RS(12,8) decode e=2 256KiB", 8, 2, 262144, 512, 12});
+    sweep<8, 4>(Shape{"RS(12,8) encode 256KiB", 8, 4, 262144, 512, 12});
+    sweep<4, 2>(Shape{"RS(6,4) encode 1KiB", 4, 2, 1024, 262144, 6});
+    sweep<4, 2>(Shape{"RS(6,4) encode 4KiB", 4, 2, 4096, 65536, 6});
+    sweep<4, 2>(Shape{"RS(6,4) encode 1MiB", 4, 2, 1048576, 256, 6});
+    sweep<4, 1>(Shape{"RS(6,4) decode e=1 1KiB", 4, 1, 1024, 262144, 6});
+    return 0;
+}
