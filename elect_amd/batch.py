@@ -92,7 +92,13 @@ def partition_by_bytes(sizes, world: int, rank: int):
         return 0, 0
     cum = np.concatenate([[0], np.cumsum(sizes)])
     total = cum[-1]
-    bounds = [int(np.searchsorted(cum, total * r / world, side="left")) for r in range(world + 1)]
+    bounds = []
+    for r in range(world + 1):
+        target = total * r / world
+        i = int(np.searchsorted(cum, target, side="left"))
+        if 0 < i <= sizes.size and target - cum[i - 1] < cum[i] - target:
+            i -= 1  # nearer boundary: ranks differ by at most one stripe's bytes
+        bounds.append(i)
     bounds[0], bounds[-1] = 0, sizes.size
     for i in range(1, world + 1):
         bounds[i] = max(bounds[i], bounds[i - 1])
