@@ -1,0 +1,114 @@
+"""GPU against the committed golden fixtures (tests/golden/*.json) directly —
+not through the oracle — so a GPU/oracle drift and an oracle change both show.
+PARITY UNPINNED vs ISA-L itself: see tests/golden/make_golden.py."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden.make_golden import seed_of
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def digest(a):
+    b = np.ascontiguousarray(a, np.uint8).tobytes()
+    return b.hex() if len(b) <= 64 else "sha256:" + hashlib.sha256(b).hexdigest()
+
+
+def _splitmix(seed, n):
+    from oracle import ec_oracle  # input generator only (splitmix64 bytes)
+    return ec_oracle.splitmix_bytes(seed, n)
+
+
+def test_golden_encode_on_gpu(dev):
+    from elect_amd.batch import encode_batch
+    from elect_amd.coder import RSCoder
+    g = load("encode.json")
+    for c in g["cases"]:
+        k, m, L = c["k"], c["m"], c["L"]
+        coder = RSCoder(k, m)
+        assert coder.encode_matrix().tobytes().hex() == g["matrices"][f"{k},{m}"]
+        data = np.stack([_splitmix(s, L) for s in c["seeds"]])[None]
+        par = torch.zeros((1, m, L), dtype=torch.uint8, device=dev)
+        encode_batch(coder, torch.from_numpy(data).to(dev), par)
+        got = par.cpu().numpy()[0]
+        assert [digest(p) for p in got] == c["parity"], (k, m, L)
+
+
+def test_golden_decode_on_gpu(dev):
+    from elect_amd.batch import decode_batch, encode_batch
+    from elect_amd.coder import RSCoder
+    g = load("decode.json")
+    for c in g["cases"]:
+        k, m, L = c["k"], c["m"], c["L"]
+        if L == 0:
+            continue
+        coder = RSCoder(k, m)
+        tag = "elect" if "input_seeds" in c else "dec"
+        st = torch.zeros((1, k + m, L), dtype=torch.uint8, device=dev)
+        st[0, :k] = torch.from_numpy(np.stack([_splitmix(seed_of(tag, k, L, j), L) for j in range(k)])).to(dev)
+        encode_batch(coder, st[:, :k], st[:, k:])
+        out = torch.full((1, len(c["erased"]), L), 0x5A, dtype=torch.uint8, device=dev)
+        mode = 1 if c["mode"] == "strict" else 0
+        st_code = decode_batch(coder, st, c["decode_indexes"], c["erased"], out, mode=mode, inputs_by_unit=True)
+        assert st_code == c["status"]
+        assert [digest(x) for x in out.cpu().numpy()[0]] == c["outputs"], c
+
+
+def test_golden_update_on_gpu(dev):
+    from elect_amd.batch import encode_update_batch
+    from elect_amd.coder import RSCoder
+    g = load("update.json")
+    for c in g["cases"]:
+        k, m, L, t = c["k"], c["m"], c["L"], c["target"]
+        coder = RSCoder(k, m)
+        old = torch.from_numpy(_splitmix(seed_of("upd-old", k, L, t), L)[None]).to(dev)
+        new = torch.from_numpy(_splitmix(seed_of("upd-new", k, L, t), L)[None]).to(dev)
+        pin = torch.from_numpy(np.stack([_splitmix(seed_of("upd-par", k, L, t, r), L) for r in range(m)])[None]).to(dev)
+        pout = torch.zeros_like(pin)
+        encode_update_batch(coder, t, old, new, pin, pout)
+        assert [digest(p) for p in pout.cpu().numpy()[0]] == c["parity_out"], (k, m, L, t)
+
+
+def test_golden_erasure_code_test_port_on_gpu(dev):
+    """ErasureCodeTest.java:31-173 through the Java-API mirror on the GPU host path."""
+    from elect_amd.coder import ByteBuffer, ErasureCoderOptions, NativeRSDecoder, NativeRSEncoder
+    from tests.golden.java_random import JavaRandom
+    g = load("erasure_code_test.json")
+    L, k, m = g["codeLength"], 4, 2
+    rnd = JavaRandom(123)
+    data, modified = [], []
+    for _ in range(k):
+        tmp = rnd.nextBytes(L)
+        data.append(ByteBuffer.allocateDirect(L).put(tmp).rewind())
+        modified.append(ByteBuffer.allocateDirect(L).put(tmp).rewind())
+    modified[0] = ByteBuffer.allocateDirect(L).put(rnd.nextBytes(L)).rewind()
+    parity = [ByteBuffer.allocateDirect(L) for _ in range(m)]
+    second = [ByteBuffer.allocateDirect(L) for _ in range(m)]
+    upd = [ByteBuffer.allocateDirect(L) for _ in range(m)]
+    enc = NativeRSEncoder(ErasureCoderOptions(k, m))
+    dec = NativeRSDecoder(ErasureCoderOptions(k, m))
+    enc.encode(data, parity)
+    enc.encode(modified, second)
+    out1, out2 = [ByteBuffer.allocateDirect(L)], [ByteBuffer.allocateDirect(L)]
+    dec.decode([parity[0]] + data[1:], [4, 1, 2, 3], [0], out1)
+    dec.decode([second[0]] + modified[1:], [4, 1, 2, 3], [0], out2)
+    enc.encodeUpdate([data[0], modified[0]] + parity, upd, 0)
+    assert [digest(b.array()) for b in data] == g["data"]
+    assert [digest(b.array()) for b in parity] == g["parity"]
+    assert [digest(b.array()) for b in second] == g["second_parity"]
+    assert [digest(b.array()) for b in upd] == g["update_parity"]
+    assert out1[0].compareTo(data[0].rewind()) == 0          # :112
+    assert out2[0].compareTo(modified[0].rewind()) == 0      # :119
+    enc.release()
+    dec.release()

@@ -34,6 +34,7 @@ for step in "$@"; do
         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run \
             -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $? ;;
     tune) run tune 600 tools/tune/tune_apply || exit $? ;;
+    hostsweep) run hostsweep 600 python tools/tune/host_sweep.py || exit $? ;;
     configs)
         run bench_mixed 400 python bench.py --config mixed || exit $?
         run bench_rs12 400 python bench.py --config rs12 || exit $?
