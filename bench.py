@@ -126,9 +126,10 @@ def cpu_baseline(args, k, m, L):
 
 
 def host_inclusive(coder, k, m, L, stripes_total, dev):
-    """Pinned host -> H2D -> encode -> D2H, two streams; GiB/s of data."""
+    """Pinned host -> H2D -> encode -> D2H, two streams; GiB/s of data.  32 MiB
+    transfers on 2 streams were the best of tools/tune/host_sweep.py's grid."""
     from elect_amd.batch import encode_batch
-    chunk = 256  # stripes per transfer (64 MiB of data at 64 KiB chunks)
+    chunk = max(1, (32 << 20) // (k * L))  # stripes per transfer (32 MiB of data)
     nchunks = max(2, stripes_total // chunk)
     h_data = torch.randint(0, 256, (nchunks * chunk, k, L), dtype=torch.uint8).pin_memory()
     h_par = torch.empty((nchunks * chunk, m, L), dtype=torch.uint8).pin_memory()
@@ -396,7 +397,7 @@ def main():
         "verified": ok,
     }
     if rank == 0 and not args.no_host:
-        out["host_inclusive_GiB/s"] = host_inclusive(coder, k, m, L, min(B, 1024), dev)
+        out["host_inclusive_GiB/s"] = host_inclusive(coder, k, m, L, min(B, 2048), dev)
     if rank == 0 and world == 1 and not args.no_cpu:
         cb, _ = cpu_baseline(args, k, m, L)
         out["cpu_baseline"] = cb
