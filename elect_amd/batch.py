@@ -44,6 +44,18 @@ def encode_batch(coder: RSCoder, data: torch.Tensor, parity: torch.Tensor, strea
           "encode_batch")
 
 
+def encode_batch_padded(coder: RSCoder, data: torch.Tensor, lengths: torch.Tensor, parity: torch.Tensor,
+                        stream=None) -> None:
+    """encode_batch where data[s, j] holds only lengths[s, j] valid bytes (int32/uint32
+    device tensor [B, k]); the rest reads as zero and is never loaded."""
+    B, k, L = data.shape
+    if lengths.shape != (B, k) or lengths.dtype not in (torch.int32, torch.uint32) or \
+            not lengths.is_contiguous() or lengths.device != data.device:
+        raise ValueError("lengths must be a contiguous int32 [B, k] tensor on the data's device")
+    check(lib.elect_ec_encode_batch_padded(coder.handle, L, B, _shards(data), lengths.data_ptr(),
+                                           _shards(parity), _stream(stream)), "encode_batch_padded")
+
+
 def decode_batch(coder: RSCoder, inputs: torch.Tensor, decode_indexes, erased, outputs: torch.Tensor,
                  mode: int = _lib.DECODE_COMPAT, inputs_by_unit: bool = False,
                  outputs_by_unit: bool = False, stream=None) -> int:

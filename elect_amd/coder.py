@@ -230,6 +230,13 @@ class RSCoder:
         return check(lib.elect_ec_encode(self.handle, ptr_array(data_addrs), ptr_array(parity_addrs),
                                          length), "encode")
 
+    def encode_padded_host(self, data_addrs, data_lengths, parity_addrs, length: int) -> int:
+        """Encode with implicit zero padding to `length` (None address for an all-zero unit)."""
+        lens = (_lib.ctypes.c_size_t * len(data_lengths))(*[int(x) for x in data_lengths])
+        addrs = [a if a is not None else 0 for a in data_addrs]
+        return check(lib.elect_ec_encode_padded(self.handle, ptr_array(addrs), lens, ptr_array(parity_addrs),
+                                                length), "encode_padded")
+
     def encode_update_host(self, in_addrs, target: int, out_addrs, length: int) -> int:
         return check(lib.elect_ec_encode_update(self.handle, ptr_array(in_addrs), target,
                                                 ptr_array(out_addrs), length), "encodeUpdate")

@@ -118,6 +118,7 @@ struct HostOp {
     const unsigned char* const* in = nullptr;
     unsigned char* const* out = nullptr;
     uint8_t coef[elect::kern::kMaxRows * elect::kern::kMaxCols] = {};
+    const size_t* lens = nullptr;  // optional content length per input (implicit zero padding)
 };
 
 class HostEngine {
@@ -159,9 +160,22 @@ public:
             if (c >= nchunks) continue;
             const size_t o = c * step;
             const size_t n = std::min(step, len - o);
-            for (int j = 0; j < op.cols; ++j) std::memcpy(pin_in_[s] + j * pitch, op.in[j] + o, n);
-            hipError_t e = hipMemcpyAsync(d_in_[s], pin_in_[s], op.cols * pitch, hipMemcpyHostToDevice, stream_[s]);
-            if (e == hipSuccess) e = launch(op, s, pitch, n);
+            hipError_t e = hipSuccess;
+            uint32_t valid[elect::kern::kMaxCols];
+            if (op.lens) {  // copy and send only each column's valid bytes
+                for (int j = 0; j < op.cols && e == hipSuccess; ++j) {
+                    const size_t v = op.lens[j] > o ? std::min(n, op.lens[j] - o) : 0;
+                    valid[j] = static_cast<uint32_t>(v);
+                    if (v == 0) continue;
+                    std::memcpy(pin_in_[s] + j * pitch, op.in[j] + o, v);
+                    e = hipMemcpyAsync(d_in_[s] + j * pitch, pin_in_[s] + j * pitch, v, hipMemcpyHostToDevice,
+                                       stream_[s]);
+                }
+            } else {
+                for (int j = 0; j < op.cols; ++j) std::memcpy(pin_in_[s] + j * pitch, op.in[j] + o, n);
+                e = hipMemcpyAsync(d_in_[s], pin_in_[s], op.cols * pitch, hipMemcpyHostToDevice, stream_[s]);
+            }
+            if (e == hipSuccess) e = launch(op, s, pitch, n, op.lens ? valid : nullptr);
             if (e == hipSuccess)
                 e = hipMemcpyAsync(pin_out_[s], d_out_[s], op.rows * pitch, hipMemcpyDeviceToHost, stream_[s]);
             if (e != hipSuccess) {
@@ -176,7 +190,7 @@ public:
     }
 
 private:
-    hipError_t launch(const HostOp& op, int s, size_t pitch, size_t n)
+    hipError_t launch(const HostOp& op, int s, size_t pitch, size_t n, const uint32_t* valid)
     {
         if (op.update) {
             UpdateParams p;
@@ -200,6 +214,10 @@ private:
         for (int j = 0; j < op.cols; ++j) p.src[j] = col(d_in_[s], pitch, j * pitch);
         for (int r = 0; r < op.rows; ++r) p.dst[r] = col(d_out_[s], pitch, r * pitch);
         std::memcpy(p.coef, op.coef, sizeof(p.coef));
+        if (valid) {
+            p.padded = true;
+            for (int j = 0; j < op.cols; ++j) p.clen[j] = valid[j];
+        }
         return elect::kern::launch_apply(p, stream_[s]);
     }
 
@@ -260,8 +278,10 @@ thread_local std::unique_ptr<HostEngine> t_engines[kMaxDevices];
 int run_host(const HostOp& op, size_t len)
 {
     if (len == 0) return ELECT_EC_OK;  // JEC/ErasureEncoder.java:41-44, JEC/ErasureDecoder.java:36-38
-    for (int j = 0; j < op.cols; ++j)
-        if (!op.in[j]) return ELECT_EC_EINVAL;
+    for (int j = 0; j < op.cols; ++j) {
+        if (op.lens && op.lens[j] > len) return ELECT_EC_EINVAL;
+        if (!op.in[j] && !(op.lens && op.lens[j] == 0)) return ELECT_EC_EINVAL;
+    }
     for (int r = 0; r < op.rows; ++r)
         if (!op.out[r]) return ELECT_EC_EINVAL;
     int ndev = 0;
@@ -369,6 +389,21 @@ int elect_ec_encode(const elect_ec_coder* coder, const unsigned char* const* dat
     return run_host(op, chunk_size);
 }
 
+int elect_ec_encode_padded(const elect_ec_coder* coder, const unsigned char* const* data_units,
+                           const size_t* data_lengths, unsigned char* const* parity_units, size_t chunk_size)
+{
+    if (!valid_coder(coder) || !data_units || !data_lengths || !parity_units) return ELECT_EC_EINVAL;
+    if (chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
+    HostOp op;
+    op.cols = coder->k;
+    op.rows = coder->m;
+    op.in = data_units;
+    op.out = parity_units;
+    op.lens = data_lengths;
+    for (int r = 0; r < coder->m; ++r) std::memcpy(op.coef + r * op.cols, parity_row(coder, r), coder->k);
+    return run_host(op, chunk_size);
+}
+
 int elect_ec_encode_update(const elect_ec_coder* coder, const unsigned char* const* old_new_parity,
                            int target_data_index, unsigned char* const* new_parity_units, size_t chunk_size)
 {
@@ -414,6 +449,29 @@ int elect_ec_encode_batch(const elect_ec_coder* coder, size_t chunk_size, size_t
     p.stripes = num_stripes;
     p.cols = coder->k;
     p.rows = coder->m;
+    for (int j = 0; j < p.cols; ++j) p.src[j] = col(data.base, data.stripe_stride, j * data.shard_stride);
+    for (int r = 0; r < p.rows; ++r) {
+        p.dst[r] = col(parity.base, parity.stripe_stride, r * parity.shard_stride);
+        std::memcpy(p.coef + r * p.cols, parity_row(coder, r), coder->k);
+    }
+    return map_hip(elect::kern::launch_apply(p, as_stream(stream)));
+}
+
+int elect_ec_encode_batch_padded(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                                 elect_ec_shards data, const uint32_t* data_lengths, elect_ec_shards parity,
+                                 void* stream)
+{
+    if (!valid_coder(coder) || !data_lengths) return ELECT_EC_EINVAL;
+    if (chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
+    if (chunk_size == 0 || num_stripes == 0) return ELECT_EC_OK;
+    if (!data.base || !parity.base) return ELECT_EC_EINVAL;
+    ApplyParams p;
+    p.len = chunk_size;
+    p.stripes = num_stripes;
+    p.cols = coder->k;
+    p.rows = coder->m;
+    p.padded = true;
+    p.lens = data_lengths;
     for (int j = 0; j < p.cols; ++j) p.src[j] = col(data.base, data.stripe_stride, j * data.shard_stride);
     for (int r = 0; r < p.rows; ++r) {
         p.dst[r] = col(parity.base, parity.stripe_stride, r * parity.shard_stride);

@@ -111,6 +111,32 @@ __device__ __forceinline__ void store_nt(uint8_t* p, const uint4& v)
     __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
 }
 
+// Partial segments (padded launches only): n < 16 valid bytes, zero filled.
+__device__ __forceinline__ uint4 load_partial(const uint8_t* p, uint32_t n)
+{
+    uint4 v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            if (static_cast<uint32_t>(4 * w + b) < n) x |= static_cast<uint32_t>(p[4 * w + b]) << (8 * b);
+        set_word(v, w, x);
+    }
+    return v;
+}
+
+__device__ __forceinline__ void store_partial(uint8_t* p, const uint4& v, uint32_t n)
+{
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t x = lane_word(v, w);
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            if (static_cast<uint32_t>(4 * w + b) < n) p[4 * w + b] = static_cast<uint8_t>(x >> (8 * b));
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Fast path: K source columns, R output rows, one 16-byte segment per lane.
 // The byte-shuffle tables (5 dwords per coefficient) are staged in LDS, padded
@@ -128,12 +154,17 @@ struct FastArgs {
     uint32_t total;  // segments in this launch (< 2^31)
     uint32_t magic;
     uint32_t shift;
+    // padded launches only
+    uint64_t len;            // bytes per shard (the last segment may be partial)
+    const uint32_t* lens;    // [stripe][lstride] content lengths, or null -> clen
+    uint32_t lstride;
+    uint32_t clen[K];
     gf::PermTable tab[R][K];
 };
 
 constexpr int kTabStride = 8;  // dwords per coefficient in LDS
 
-template <int K, int R>
+template <int K, int R, bool PAD>
 __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
@@ -154,7 +185,17 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 
     uint4 x[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + stripe * a.ss[j] + off);
+    for (int j = 0; j < K; ++j) {
+        const uint8_t* p = a.sp[j] + stripe * a.ss[j] + off;
+        if (!PAD) {
+            x[j] = load_nt(p);
+        } else {
+            const uint64_t valid = a.lens ? a.lens[static_cast<uint64_t>(stripe) * a.lstride + j] : a.clen[j];
+            if (off + 16 <= valid) x[j] = load_nt(p);
+            else if (off >= valid) x[j] = make_uint4(0, 0, 0, 0);
+            else x[j] = load_partial(p, static_cast<uint32_t>(valid - off));
+        }
+    }
 
     uint4 acc[R];
 #pragma unroll
@@ -180,24 +221,34 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
             }
         }
     }
+    if (!PAD || off + 16 <= a.len) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) store_nt(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
+        for (int r = 0; r < R; ++r) store_nt(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
+    } else {
+        const uint32_t n = static_cast<uint32_t>(a.len - off);
+#pragma unroll
+        for (int r = 0; r < R; ++r) store_partial(a.dp[r] + stripe * a.ds[r] + off, acc[r], n);
+    }
 }
 
 // Small chunks (<= 4 KiB per shard) ran 3-4 % faster with 128-thread blocks.
 inline int block_for(uint64_t len) { return len <= 4096 ? 128 : kBlock; }
 
-template <int K, int R>
+template <int K, int R, bool PAD>
 hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
 {
     FastArgs<K, R> a{};
-    const uint64_t segs64 = p.len / 16;
+    // padded: every segment incl. a partial last one; else whole segments only
+    const uint64_t segs64 = PAD ? (p.len + 15) / 16 : p.len / 16;
     if (segs64 == 0) return hipSuccess;
     if (segs64 > kMaxIndex) return hipErrorInvalidValue;
     a.segs = static_cast<uint32_t>(segs64);
     const Magic mg = make_magic(a.segs);
     a.magic = mg.m;
     a.shift = mg.p;
+    a.len = p.len;
+    a.lstride = static_cast<uint32_t>(p.cols);
+    for (int j = 0; j < K; ++j) a.clen[j] = p.clen[j];
     for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(p.coef[(r0 + r) * p.cols + j]);
     const int block = block_for(p.len);
@@ -212,9 +263,10 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             a.dp[r] = const_cast<uint8_t*>(p.dst[r0 + r].ptr) + s0 * p.dst[r0 + r].stride;
             a.ds[r] = p.dst[r0 + r].stride;
         }
+        a.lens = p.lens ? p.lens + s0 * p.cols : nullptr;
         a.total = static_cast<uint32_t>(ns * segs64);
         const uint32_t grid = (a.total + block - 1) / block;
-        hipLaunchKernelGGL((gf_apply_x16<K, R>), dim3(grid), dim3(block), 0, stream, a);
+        hipLaunchKernelGGL((gf_apply_x16<K, R, PAD>), dim3(grid), dim3(block), 0, stream, a);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -223,10 +275,11 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
 
 using FastFn = hipError_t (*)(const ApplyParams&, int, hipStream_t);
 
-template <int K>
+template <int K, bool PAD = false>
 constexpr std::array<FastFn, kFastRows> fast_row_fns()
 {
-    return {&launch_fast_kr<K, 1>, &launch_fast_kr<K, 2>, &launch_fast_kr<K, 3>, &launch_fast_kr<K, 4>};
+    return {&launch_fast_kr<K, 1, PAD>, &launch_fast_kr<K, 2, PAD>, &launch_fast_kr<K, 3, PAD>,
+            &launch_fast_kr<K, 4, PAD>};
 }
 
 const std::array<std::array<FastFn, kFastRows>, kMaxCols> kFast = {
@@ -234,6 +287,14 @@ const std::array<std::array<FastFn, kFastRows>, kMaxCols> kFast = {
     fast_row_fns<5>(),  fast_row_fns<6>(),  fast_row_fns<7>(),  fast_row_fns<8>(),
     fast_row_fns<9>(),  fast_row_fns<10>(), fast_row_fns<11>(), fast_row_fns<12>(),
     fast_row_fns<13>(), fast_row_fns<14>(), fast_row_fns<15>(), fast_row_fns<16>()};
+
+// Padded variants exist for up to ELECT_EC_MAX_DATA_UNITS (10) columns: the
+// encode shapes and ELECT's decode (k survivors).
+constexpr int kMaxPadCols = 10;
+const std::array<std::array<FastFn, kFastRows>, kMaxPadCols> kFastPad = {
+    fast_row_fns<1, true>(), fast_row_fns<2, true>(), fast_row_fns<3, true>(), fast_row_fns<4, true>(),
+    fast_row_fns<5, true>(), fast_row_fns<6, true>(), fast_row_fns<7, true>(), fast_row_fns<8, true>(),
+    fast_row_fns<9, true>(), fast_row_fns<10, true>()};
 
 // ---------------------------------------------------------------------------
 // Byte-granular path: any alignment, any (cols, rows) up to 16 x 16.
@@ -250,6 +311,10 @@ struct GenericArgs {
     int cols;
     int rows;
     uint8_t coef[kMaxRows * kMaxCols];
+    const uint32_t* lens;  // padded: [stripe][cols] content lengths, or null -> clen
+    uint32_t clen[kMaxCols];
+    int padded;
+    uint32_t col_base;     // byte offset of this launch window inside the shard
 };
 
 __constant__ uint8_t d_exp[512];
@@ -264,7 +329,13 @@ __global__ __launch_bounds__(kBlock) void gf_apply_bytes(const GenericArgs a)
     uint8_t lx[kMaxCols];
     bool nz[kMaxCols];
     for (int j = 0; j < a.cols; ++j) {
-        const uint8_t v = a.sp[j][s * a.ss[j] + i];
+        uint8_t v = 0;
+        if (a.padded) {
+            const uint32_t valid = a.lens ? a.lens[static_cast<uint64_t>(s) * a.cols + j] : a.clen[j];
+            if (a.col_base + i < valid) v = a.sp[j][s * a.ss[j] + i];
+        } else {
+            v = a.sp[j][s * a.ss[j] + i];
+        }
         nz[j] = v != 0;
         lx[j] = d_log[v];
     }
@@ -300,6 +371,9 @@ hipError_t launch_bytes(const ApplyParams& p, hipStream_t stream)
     a.cols = p.cols;
     a.rows = p.rows;
     std::copy(p.coef, p.coef + kMaxRows * kMaxCols, a.coef);
+    a.padded = p.padded ? 1 : 0;
+    std::copy(p.clen, p.clen + kMaxCols, a.clen);
+    a.col_base = p.padded ? p.col_base : 0;
     const Magic mg = make_magic(a.len);
     a.magic = mg.m;
     a.shift = mg.p;
@@ -314,6 +388,7 @@ hipError_t launch_bytes(const ApplyParams& p, hipStream_t stream)
             a.dp[r] = const_cast<uint8_t*>(p.dst[r].ptr) + s0 * p.dst[r].stride;
             a.ds[r] = p.dst[r].stride;
         }
+        a.lens = p.lens ? p.lens + s0 * p.cols : nullptr;
         a.total = static_cast<uint32_t>(ns * p.len);
         const uint32_t grid = (a.total + kBlock - 1) / kBlock;
         hipLaunchKernelGGL(gf_apply_bytes, dim3(grid), dim3(kBlock), 0, stream, a);
@@ -450,6 +525,17 @@ hipError_t launch_apply(const ApplyParams& p, hipStream_t stream)
 {
     if (p.cols < 1 || p.cols > kMaxCols || p.rows < 1 || p.rows > kMaxRows) return hipErrorInvalidValue;
     if (p.len == 0 || p.stripes == 0) return hipSuccess;
+    if (p.padded) {
+        for (int j = 0; j < p.cols; ++j)
+            if (!p.lens && p.clen[j] > p.len) return hipErrorInvalidValue;
+        if (!apply_is_aligned(p) || p.cols > kMaxPadCols) return launch_bytes(p, stream);
+        for (int r0 = 0; r0 < p.rows; r0 += kFastRows) {
+            const int nr = std::min(kFastRows, p.rows - r0);
+            const hipError_t e = kFastPad[p.cols - 1][nr - 1](p, r0, stream);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
     if (!apply_is_aligned(p)) return launch_bytes(p, stream);
     for (int r0 = 0; r0 < p.rows; r0 += kFastRows) {
         const int nr = std::min(kFastRows, p.rows - r0);

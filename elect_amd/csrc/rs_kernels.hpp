@@ -36,6 +36,15 @@ struct ApplyParams {
     int cols = 0;
     int rows = 0;
     uint8_t coef[kMaxRows * kMaxCols] = {};  // rows x cols, row-major
+    // Implicit zero padding (padded == true): column j of stripe s holds only
+    // lens[s * cols + j] valid bytes (device array), or clen[j] for every
+    // stripe when lens is null; bytes past that read as zero.  This is ELECT's
+    // zero fill up to codeLength (ECMessageVerbHandler.java:292-310) and its
+    // all-zero filler chunks (:174-184), without storing or reading the zeros.
+    bool padded = false;
+    const uint32_t* lens = nullptr;
+    uint32_t clen[kMaxCols] = {};
+    uint32_t col_base = 0;  // internal: byte offset of a launch window inside the shard
 };
 
 // par_out[r] = par_in[r] ^ coef[r] * (old ^ new): ec_encode_data_update with

@@ -116,6 +116,15 @@ int elect_ec_decode(const elect_ec_coder* coder, const unsigned char* const* inp
                     const int* decode_indexes, const int* erased_indexes, int num_erased,
                     unsigned char* const* outputs, size_t chunk_size, int mode);
 
+/* Implicit zero padding (host memory): data unit j holds only data_lengths[j]
+ * <= chunk_size valid bytes and reads as zero past that, exactly like ELECT's
+ * zero fill up to codeLength (JEC/net/ECMessageVerbHandler.java:292-310);
+ * data_units[j] may be NULL when data_lengths[j] == 0 (ELECT's all-zero filler
+ * chunks, :174-184).  Only the valid bytes are copied and sent to the device. */
+int elect_ec_encode_padded(const elect_ec_coder* coder, const unsigned char* const* data_units,
+                           const size_t* data_lengths, unsigned char* const* parity_units,
+                           size_t chunk_size);
+
 /* ---- device resident, batched, stream ordered ----
  * Many stripes per launch.  All pointers are device pointers on the calling
  * thread's current device; the call only enqueues work on `stream`.  16-byte
@@ -127,6 +136,12 @@ int elect_ec_decode_batch(const elect_ec_coder* coder, size_t chunk_size, size_t
                           elect_ec_shards inputs, const int* decode_indexes,
                           const int* erased_indexes, int num_erased, elect_ec_shards outputs,
                           unsigned flags, int mode, void* stream);
+/* Zero-padded batch encode: data_lengths is a DEVICE array [num_stripes][k] of
+ * uint32 content lengths (each <= chunk_size); bytes past a unit's length read
+ * as zero and are never loaded. */
+int elect_ec_encode_batch_padded(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                                 elect_ec_shards data, const uint32_t* data_lengths,
+                                 elect_ec_shards parity, void* stream);
 /* parity_out[r] = parity_in[r] ^ E[k+r][target] * (old ^ new) for each stripe. */
 int elect_ec_encode_update_batch(const elect_ec_coder* coder, size_t chunk_size,
                                  size_t num_stripes, int target_data_index,
