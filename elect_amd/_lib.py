@@ -78,6 +78,8 @@ SIGNATURES = [
     ("elect_ec_encode_update", ctypes.c_int, [_cp, _u8pp, ctypes.c_int, _u8pp, ctypes.c_size_t]),
     ("elect_ec_encode_padded", ctypes.c_int, [_cp, _u8pp, ctypes.POINTER(ctypes.c_size_t), _u8pp,
                                               ctypes.c_size_t]),
+    ("elect_ec_encode_hashed", ctypes.c_int, [_cp, _u8pp, _u8pp, ctypes.c_size_t,
+                                              ctypes.POINTER(ctypes.c_int32)]),
     ("elect_ec_decode", ctypes.c_int, [_cp, _u8pp, _ip, _ip, ctypes.c_int, _u8pp, ctypes.c_size_t,
                                        ctypes.c_int]),
     ("elect_ec_encode_batch", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, Shards, Shards, _cp]),
@@ -85,6 +87,8 @@ SIGNATURES = [
                                              ctypes.c_int, Shards, ctypes.c_uint, ctypes.c_int, _cp]),
     ("elect_ec_encode_batch_padded", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, Shards, _cp,
                                                     Shards, _cp]),
+    ("elect_ec_encode_batch_hashed", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, Shards, Shards,
+                                                    _cp, _cp]),
     ("elect_ec_encode_update_batch", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                                                     ColumnT, ColumnT, Shards, Shards, _cp]),
     ("elect_ec_apply_batch", ctypes.c_int, [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,

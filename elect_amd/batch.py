@@ -44,6 +44,17 @@ def encode_batch(coder: RSCoder, data: torch.Tensor, parity: torch.Tensor, strea
           "encode_batch")
 
 
+def encode_batch_hashed(coder: RSCoder, data: torch.Tensor, parity: torch.Tensor, hashes: torch.Tensor,
+                        stream=None) -> None:
+    """encode_batch that also writes every parity unit's java.nio.ByteBuffer.hashCode()
+    into hashes (int32 device tensor [B, m])."""
+    B, k, L = data.shape
+    if hashes.shape != (B, coder.m) or hashes.dtype != torch.int32 or not hashes.is_contiguous():
+        raise ValueError("hashes must be a contiguous int32 [B, m] tensor")
+    check(lib.elect_ec_encode_batch_hashed(coder.handle, L, B, _shards(data), _shards(parity), hashes.data_ptr(),
+                                           _stream(stream)), "encode_batch_hashed")
+
+
 def encode_batch_padded(coder: RSCoder, data: torch.Tensor, lengths: torch.Tensor, parity: torch.Tensor,
                         stream=None) -> None:
     """encode_batch where data[s, j] holds only lengths[s, j] valid bytes (int32/uint32

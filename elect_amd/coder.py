@@ -168,14 +168,25 @@ class ByteBuffer:
 
     def hashCode(self) -> int:
         """java.nio.ByteBuffer.hashCode: h = 1; for i = limit-1 .. position: h = 31*h + b[i]
-        over signed bytes, wrapped to int32 (used for parity naming,
-        ECMessageVerbHandler.java:326-329)."""
-        b = self.view().view(np.int8).astype(np.int64)[::-1]
-        h = 1
-        mod = 1 << 32
-        for x in b:  # small buffers only; the device path fuses this later
-            h = (31 * h + int(x)) % mod
-        return h - mod if h >= 1 << 31 else h
+        over signed bytes, as int32 (ELECT names parity by it,
+        ECMessageVerbHandler.java:326-329).  Closed form: 31^n + sum b[i]*31^i mod 2^32."""
+        return java_bytebuffer_hash(self.view())
+
+
+def java_bytebuffer_hash(b: np.ndarray) -> int:
+    """Closed form of java.nio.ByteBuffer.hashCode over the bytes b (signed), int32."""
+    b = np.ascontiguousarray(b, np.uint8)
+    n = b.size
+    with np.errstate(over="ignore"):
+        pw = np.empty(n + 1, np.uint32)
+        pw[0] = 1
+        if n:
+            pw[1:] = 31
+            pw = np.cumprod(pw, dtype=np.uint32)
+        sb = b.view(np.int8).astype(np.int64).astype(np.uint32)
+        h = (np.sum(sb * pw[:n], dtype=np.uint32) + pw[n]).astype(np.uint32)
+    h = int(h)
+    return h - (1 << 32) if h >= 1 << 31 else h
 
 
 # ---------------------------------------------------------------------------
@@ -229,6 +240,13 @@ class RSCoder:
     def encode_host(self, data_addrs, parity_addrs, length: int) -> int:
         return check(lib.elect_ec_encode(self.handle, ptr_array(data_addrs), ptr_array(parity_addrs),
                                          length), "encode")
+
+    def encode_hashed_host(self, data_addrs, parity_addrs, length: int) -> list:
+        """Encode and return each parity unit's java.nio.ByteBuffer.hashCode() (fused)."""
+        h = (_lib.ctypes.c_int32 * self.m)()
+        check(lib.elect_ec_encode_hashed(self.handle, ptr_array(data_addrs), ptr_array(parity_addrs), length, h),
+              "encode_hashed")
+        return list(h)
 
     def encode_padded_host(self, data_addrs, data_lengths, parity_addrs, length: int) -> int:
         """Encode with implicit zero padding to `length` (None address for an all-zero unit)."""

@@ -119,6 +119,7 @@ struct HostOp {
     unsigned char* const* out = nullptr;
     uint8_t coef[elect::kern::kMaxRows * elect::kern::kMaxCols] = {};
     const size_t* lens = nullptr;  // optional content length per input (implicit zero padding)
+    int32_t* hashes = nullptr;     // optional host output: ByteBuffer.hashCode() per output row
 };
 
 class HostEngine {
@@ -136,6 +137,7 @@ public:
             if (d_in_[s]) (void)hipFree(d_in_[s]);
             if (d_out_[s]) (void)hipFree(d_out_[s]);
         }
+        if (d_hash_) (void)hipFree(d_hash_);
     }
 
     int run(const HostOp& op, size_t len)
@@ -145,6 +147,12 @@ public:
         int rc = reserve(static_cast<size_t>(op.cols) * pitch, static_cast<size_t>(op.rows) * pitch);
         if (rc != ELECT_EC_OK) return rc;
         const size_t nchunks = (len + step - 1) / step;
+        if (op.hashes) {  // every chunk's kernel adds into d_hash_; start from 31^len
+            hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_hash_),
+                                             static_cast<int>(elect::kern::pow31(len)), op.rows, stream_[0]);
+            if (e == hipSuccess) e = hipStreamSynchronize(stream_[0]);
+            if (e != hipSuccess) return map_hip(e);
+        }
         size_t pending[kSlots] = {};
         bool busy[kSlots] = {};
         for (size_t c = 0; c < nchunks + kSlots; ++c) {
@@ -175,7 +183,7 @@ public:
                 for (int j = 0; j < op.cols; ++j) std::memcpy(pin_in_[s] + j * pitch, op.in[j] + o, n);
                 e = hipMemcpyAsync(d_in_[s], pin_in_[s], op.cols * pitch, hipMemcpyHostToDevice, stream_[s]);
             }
-            if (e == hipSuccess) e = launch(op, s, pitch, n, op.lens ? valid : nullptr);
+            if (e == hipSuccess) e = launch(op, s, pitch, n, op.lens ? valid : nullptr, o);
             if (e == hipSuccess)
                 e = hipMemcpyAsync(pin_out_[s], d_out_[s], op.rows * pitch, hipMemcpyDeviceToHost, stream_[s]);
             if (e != hipSuccess) {
@@ -186,11 +194,15 @@ public:
             pending[s] = c;
             busy[s] = true;
         }
+        if (op.hashes) {
+            const hipError_t e = hipMemcpy(op.hashes, d_hash_, op.rows * sizeof(int32_t), hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return map_hip(e);
+        }
         return ELECT_EC_OK;
     }
 
 private:
-    hipError_t launch(const HostOp& op, int s, size_t pitch, size_t n, const uint32_t* valid)
+    hipError_t launch(const HostOp& op, int s, size_t pitch, size_t n, const uint32_t* valid, size_t offset)
     {
         if (op.update) {
             UpdateParams p;
@@ -218,6 +230,11 @@ private:
             p.padded = true;
             for (int j = 0; j < op.cols; ++j) p.clen[j] = valid[j];
         }
+        if (op.hashes) {
+            p.hashes = d_hash_;
+            p.hash_stride = static_cast<uint32_t>(op.rows);
+            p.hash_base = offset;
+        }
         return elect::kern::launch_apply(p, stream_[s]);
     }
 
@@ -228,6 +245,8 @@ private:
                 const hipError_t e = hipStreamCreateWithFlags(&stream_[s], hipStreamNonBlocking);
                 if (e != hipSuccess) return map_hip(e);
             }
+            const hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_hash_), elect::kern::kMaxRows * sizeof(int32_t));
+            if (e != hipSuccess) return map_hip(e);
         }
         if (in_bytes > cap_in_) {
             for (int s = 0; s < kSlots; ++s) {
@@ -270,6 +289,7 @@ private:
     uint8_t* d_out_[kSlots] = {};
     size_t cap_in_ = 0;
     size_t cap_out_ = 0;
+    int32_t* d_hash_ = nullptr;
 };
 
 constexpr int kMaxDevices = 64;
@@ -404,6 +424,24 @@ int elect_ec_encode_padded(const elect_ec_coder* coder, const unsigned char* con
     return run_host(op, chunk_size);
 }
 
+int elect_ec_encode_hashed(const elect_ec_coder* coder, const unsigned char* const* data_units,
+                           unsigned char* const* parity_units, size_t chunk_size, int32_t* hashes)
+{
+    if (!valid_coder(coder) || !data_units || !parity_units || !hashes) return ELECT_EC_EINVAL;
+    if (chunk_size == 0) {  // hashCode of an empty buffer is 1
+        for (int r = 0; r < coder->m; ++r) hashes[r] = 1;
+        return ELECT_EC_OK;
+    }
+    HostOp op;
+    op.cols = coder->k;
+    op.rows = coder->m;
+    op.in = data_units;
+    op.out = parity_units;
+    op.hashes = hashes;
+    for (int r = 0; r < coder->m; ++r) std::memcpy(op.coef + r * op.cols, parity_row(coder, r), coder->k);
+    return run_host(op, chunk_size);
+}
+
 int elect_ec_encode_update(const elect_ec_coder* coder, const unsigned char* const* old_new_parity,
                            int target_data_index, unsigned char* const* new_parity_units, size_t chunk_size)
 {
@@ -472,6 +510,31 @@ int elect_ec_encode_batch_padded(const elect_ec_coder* coder, size_t chunk_size,
     p.rows = coder->m;
     p.padded = true;
     p.lens = data_lengths;
+    for (int j = 0; j < p.cols; ++j) p.src[j] = col(data.base, data.stripe_stride, j * data.shard_stride);
+    for (int r = 0; r < p.rows; ++r) {
+        p.dst[r] = col(parity.base, parity.stripe_stride, r * parity.shard_stride);
+        std::memcpy(p.coef + r * p.cols, parity_row(coder, r), coder->k);
+    }
+    return map_hip(elect::kern::launch_apply(p, as_stream(stream)));
+}
+
+int elect_ec_encode_batch_hashed(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                                 elect_ec_shards data, elect_ec_shards parity, int32_t* d_hashes, void* stream)
+{
+    if (!valid_coder(coder) || !d_hashes) return ELECT_EC_EINVAL;
+    if (num_stripes == 0) return ELECT_EC_OK;
+    if (chunk_size > 0 && (!data.base || !parity.base)) return ELECT_EC_EINVAL;
+    hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_hashes),
+                                     static_cast<int>(elect::kern::pow31(chunk_size)),
+                                     num_stripes * static_cast<size_t>(coder->m), as_stream(stream));
+    if (e != hipSuccess || chunk_size == 0) return map_hip(e);
+    ApplyParams p;
+    p.len = chunk_size;
+    p.stripes = num_stripes;
+    p.cols = coder->k;
+    p.rows = coder->m;
+    p.hashes = d_hashes;
+    p.hash_stride = static_cast<uint32_t>(coder->m);
     for (int j = 0; j < p.cols; ++j) p.src[j] = col(data.base, data.stripe_stride, j * data.shard_stride);
     for (int r = 0; r < p.rows; ++r) {
         p.dst[r] = col(parity.base, parity.stripe_stride, r * parity.shard_stride);

@@ -138,6 +138,38 @@ __device__ __forceinline__ void store_partial(uint8_t* p, const uint4& v, uint32
 }
 
 // ---------------------------------------------------------------------------
+// Fused parity hash (java.nio.ByteBuffer.hashCode), see ApplyParams::hashes.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t dpow31(uint64_t e)
+{
+    uint32_t r = 1, b = 31;
+    for (; e; e >>= 1, b *= b)
+        if (e & 1) r *= b;
+    return r;
+}
+
+// sum_t sb[t] * 31^t over the 16 bytes of a segment (Horner from the top byte).
+__device__ __forceinline__ uint32_t horner31(const uint4& v)
+{
+    uint32_t h = 0;
+#pragma unroll
+    for (int w = 3; w >= 0; --w) {
+        const uint32_t x = lane_word(v, w);
+#pragma unroll
+        for (int b = 3; b >= 0; --b)
+            h = h * 31u + static_cast<uint32_t>(static_cast<int32_t>(x << (24 - 8 * b)) >> 24);
+    }
+    return h;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d, 64));
+    return v;
+}
+
+// ---------------------------------------------------------------------------
 // Fast path: K source columns, R output rows, one 16-byte segment per lane.
 // The byte-shuffle tables (5 dwords per coefficient) are staged in LDS, padded
 // to 8 dwords so one ds_read_b128 + one ds_read_b32 (wave-uniform address,
@@ -159,6 +191,9 @@ struct FastArgs {
     const uint32_t* lens;    // [stripe][lstride] content lengths, or null -> clen
     uint32_t lstride;
     uint32_t clen[K];
+    int32_t* hashes;        // optional parity hashes, [stripe][hstride] (row r at +r)
+    uint32_t hstride;
+    uint64_t hbase;
     gf::PermTable tab[R][K];
 };
 
@@ -229,6 +264,43 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 #pragma unroll
         for (int r = 0; r < R; ++r) store_partial(a.dp[r] + stripe * a.ds[r] + off, acc[r], n);
     }
+
+    if (a.hashes) {  // fused parity hash: one integer atomic per wave and row
+        if (PAD && off + 16 > a.len) {  // a partial last segment: zero the bytes past len
+            const uint32_t n = static_cast<uint32_t>(a.len - off);
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const int lo = 4 * w;
+                    const uint32_t keep = n >= static_cast<uint32_t>(lo + 4) ? 0xFFFFFFFFu
+                                          : n <= static_cast<uint32_t>(lo) ? 0u : ((1u << (8 * (n - lo))) - 1u);
+                    set_word(acc[r], w, lane_word(acc[r], w) & keep);
+                }
+        }
+        const uint32_t first = __builtin_amdgcn_readfirstlane(idx);
+        const uint32_t last = first + 63;
+        const uint32_t s_first = static_cast<uint32_t>((static_cast<uint64_t>(first) * a.magic) >> a.shift);
+        const uint32_t s_last = static_cast<uint32_t>((static_cast<uint64_t>(last) * a.magic) >> a.shift);
+        const bool whole_wave = last < a.total && s_first == s_last;  // wave-uniform
+        if (whole_wave) {
+            const uint32_t seg0 = first - s_first * a.segs;
+            const uint32_t p0 = dpow31(a.hbase + static_cast<uint64_t>(seg0) * 16);
+            const uint32_t pl = dpow31(16u * (threadIdx.x & 63u));
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t sum = wave_sum(horner31(acc[r]) * pl * p0);
+                if ((threadIdx.x & 63u) == 0)
+                    atomicAdd(reinterpret_cast<unsigned*>(a.hashes) + static_cast<uint64_t>(stripe) * a.hstride + r, sum);
+            }
+        } else {
+            const uint32_t p = dpow31(a.hbase + off);
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                atomicAdd(reinterpret_cast<unsigned*>(a.hashes) + static_cast<uint64_t>(stripe) * a.hstride + r,
+                          horner31(acc[r]) * p);
+        }
+    }
 }
 
 // Small chunks (<= 4 KiB per shard) ran 3-4 % faster with 128-thread blocks.
@@ -249,6 +321,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     a.len = p.len;
     a.lstride = static_cast<uint32_t>(p.cols);
     for (int j = 0; j < K; ++j) a.clen[j] = p.clen[j];
+    a.hstride = p.hash_stride;
+    a.hbase = p.hash_base;
     for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(p.coef[(r0 + r) * p.cols + j]);
     const int block = block_for(p.len);
@@ -264,6 +338,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             a.ds[r] = p.dst[r0 + r].stride;
         }
         a.lens = p.lens ? p.lens + s0 * p.cols : nullptr;
+        a.hashes = p.hashes ? p.hashes + s0 * p.hash_stride + r0 : nullptr;
         a.total = static_cast<uint32_t>(ns * segs64);
         const uint32_t grid = (a.total + block - 1) / block;
         hipLaunchKernelGGL((gf_apply_x16<K, R, PAD>), dim3(grid), dim3(block), 0, stream, a);
@@ -315,6 +390,9 @@ struct GenericArgs {
     uint32_t clen[kMaxCols];
     int padded;
     uint32_t col_base;     // byte offset of this launch window inside the shard
+    int32_t* hashes;       // optional parity hashes [stripe][hstride]
+    uint32_t hstride;
+    uint64_t hbase;        // hash offset of byte 0 of this window
 };
 
 __constant__ uint8_t d_exp[512];
@@ -346,6 +424,9 @@ __global__ __launch_bounds__(kBlock) void gf_apply_bytes(const GenericArgs a)
             if (c != 0 && nz[j]) acc ^= d_exp[d_log[c] + lx[j]];
         }
         a.dp[r][s * a.ds[r] + i] = acc;
+        if (a.hashes)
+            atomicAdd(reinterpret_cast<unsigned*>(a.hashes) + static_cast<uint64_t>(s) * a.hstride + r,
+                      static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(acc))) * dpow31(a.hbase + i));
     }
 }
 
@@ -374,6 +455,8 @@ hipError_t launch_bytes(const ApplyParams& p, hipStream_t stream)
     a.padded = p.padded ? 1 : 0;
     std::copy(p.clen, p.clen + kMaxCols, a.clen);
     a.col_base = p.padded ? p.col_base : 0;
+    a.hstride = p.hash_stride;
+    a.hbase = p.hash_base;
     const Magic mg = make_magic(a.len);
     a.magic = mg.m;
     a.shift = mg.p;
@@ -389,6 +472,7 @@ hipError_t launch_bytes(const ApplyParams& p, hipStream_t stream)
             a.ds[r] = p.dst[r].stride;
         }
         a.lens = p.lens ? p.lens + s0 * p.cols : nullptr;
+        a.hashes = p.hashes ? p.hashes + s0 * p.hash_stride : nullptr;
         a.total = static_cast<uint32_t>(ns * p.len);
         const uint32_t grid = (a.total + kBlock - 1) / kBlock;
         hipLaunchKernelGGL(gf_apply_bytes, dim3(grid), dim3(kBlock), 0, stream, a);
@@ -487,6 +571,7 @@ ApplyParams tail_of(const ApplyParams& p)
     for (int j = 0; j < p.cols; ++j) q.src[j].ptr = p.src[j].ptr + body;
     for (int r = 0; r < p.rows; ++r) q.dst[r].ptr = p.dst[r].ptr + body;
     q.len = p.len - body;
+    q.hash_base = p.hash_base + body;
     return q;
 }
 

@@ -45,7 +45,25 @@ struct ApplyParams {
     const uint32_t* lens = nullptr;
     uint32_t clen[kMaxCols] = {};
     uint32_t col_base = 0;  // internal: byte offset of a launch window inside the shard
+    // Optional java.nio.ByteBuffer.hashCode() of every output row (ELECT names
+    // parity by it, ECMessageVerbHandler.java:326-329):
+    //   h = 31^L + sum_i sb[i] * 31^i  (mod 2^32, sb = signed byte).
+    // The kernels ADD sum_i sb[i] * 31^(hash_base + i) into hashes[s*hash_stride + r]
+    // with integer atomics (exact, order-independent); the caller initialises
+    // every entry to 31^L first.
+    int32_t* hashes = nullptr;
+    uint32_t hash_stride = 0;
+    uint64_t hash_base = 0;
 };
+
+// 31^e mod 2^32 (host side of the parity hash).
+inline uint32_t pow31(uint64_t e)
+{
+    uint32_t r = 1, b = 31;
+    for (; e; e >>= 1, b *= b)
+        if (e & 1) r *= b;
+    return r;
+}
 
 // par_out[r] = par_in[r] ^ coef[r] * (old ^ new): ec_encode_data_update with
 // ELECT's old^new folding (EC/erasure_coder.c:100-142), fused into one pass.

@@ -125,6 +125,14 @@ int elect_ec_encode_padded(const elect_ec_coder* coder, const unsigned char* con
                            const size_t* data_lengths, unsigned char* const* parity_units,
                            size_t chunk_size);
 
+/* encode + java.nio.ByteBuffer.hashCode() of every parity unit (hashes[r], int32),
+ * fused into the encode kernel.  ELECT names parity blocks by this hash right
+ * after encoding (JEC/net/ECMessageVerbHandler.java:326-329,
+ * ECParityUpdateVerbHandler.java:696-699): h = 1; for i = L-1..0: h = 31*h + b[i]
+ * over signed bytes, i.e. 31^L + sum_i b[i]*31^i mod 2^32. */
+int elect_ec_encode_hashed(const elect_ec_coder* coder, const unsigned char* const* data_units,
+                           unsigned char* const* parity_units, size_t chunk_size, int32_t* hashes);
+
 /* ---- device resident, batched, stream ordered ----
  * Many stripes per launch.  All pointers are device pointers on the calling
  * thread's current device; the call only enqueues work on `stream`.  16-byte
@@ -142,6 +150,11 @@ int elect_ec_decode_batch(const elect_ec_coder* coder, size_t chunk_size, size_t
 int elect_ec_encode_batch_padded(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
                                  elect_ec_shards data, const uint32_t* data_lengths,
                                  elect_ec_shards parity, void* stream);
+/* encode_batch + parity hashes: d_hashes is a DEVICE array [num_stripes][m] of
+ * int32, overwritten with each parity unit's ByteBuffer.hashCode(). */
+int elect_ec_encode_batch_hashed(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                                 elect_ec_shards data, elect_ec_shards parity, int32_t* d_hashes,
+                                 void* stream);
 /* parity_out[r] = parity_in[r] ^ E[k+r][target] * (old ^ new) for each stripe. */
 int elect_ec_encode_update_batch(const elect_ec_coder* coder, size_t chunk_size,
                                  size_t num_stripes, int target_data_index,

@@ -87,5 +87,19 @@ def test_bytebuffer_semantics():
     for x in reversed([0, 1, 2, 3, 4, 5, 6, 7]):
         h = (31 * h + x) & 0xFFFFFFFF
     assert b.hashCode() == (h - (1 << 32) if h >= 1 << 31 else h)
+    assert ByteBuffer.direct_from(np.array([0x80, 0xFF], np.uint8)).hashCode() == 31 * 31 + 31 * (-1) + (-128)
     w = ByteBuffer.wrap(b"\x01\x02")
     assert not w.isDirect() and w.hasArray()
+
+
+def test_java_hash_closed_form_equals_jdk_loop():
+    """The vectorised closed form used everywhere equals the JDK loop literally."""
+    from elect_amd.coder import java_bytebuffer_hash
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 2, 15, 16, 17, 100, 1031):
+        b = rng.integers(0, 256, n, dtype=np.uint8)
+        h = 1
+        for x in b[::-1].view(np.int8):
+            h = (31 * h + int(x)) & 0xFFFFFFFF
+        h = h - (1 << 32) if h >= 1 << 31 else h
+        assert java_bytebuffer_hash(b) == h

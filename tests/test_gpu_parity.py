@@ -354,3 +354,40 @@ def test_host_path_concurrent_callers(dev, oracle):
     for x in th:
         x.join()
     assert not errors, errors
+
+
+@pytest.mark.parametrize("k,m,L", [(4, 2, 65536), (4, 2, 4099), (4, 2, 1), (4, 2, 15), (8, 4, 1024),
+                                   (4, 10, 333), (3, 2, 4404020 // 64)])
+def test_encode_batch_hashed_matches_java_hashcode(dev, oracle, k, m, L):
+    """Fused parity hash == java.nio.ByteBuffer.hashCode() of each parity unit
+    (ECMessageVerbHandler.java:326-329), incl. tails, waves straddling stripes,
+    and row groups (m > 4)."""
+    from elect_amd.batch import encode_batch_hashed
+    from elect_amd.coder import RSCoder, java_bytebuffer_hash
+    rng = np.random.default_rng(L + 13 * k)
+    B = 5
+    data = _rand(rng, B, k, L)
+    par = torch.zeros((B, m, L), dtype=torch.uint8, device=dev)
+    hashes = torch.zeros((B, m), dtype=torch.int32, device=dev)
+    encode_batch_hashed(RSCoder(k, m), _to(dev, data), par, hashes)
+    got_p, got_h = par.cpu().numpy(), hashes.cpu().numpy()
+    enc = oracle.Encoder(k, m)
+    for s in range(B):
+        want = enc.encode([data[s, j] for j in range(k)])
+        for r in range(m):
+            assert np.array_equal(got_p[s, r], want[r])
+            assert int(got_h[s, r]) == java_bytebuffer_hash(want[r]), (s, r)
+
+
+def test_encode_hashed_host_path(dev, oracle):
+    from elect_amd.coder import RSCoder, java_bytebuffer_hash
+    k, m = 4, 2
+    for L in (4404020, 17, 0):
+        rng = np.random.default_rng(L)
+        d = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+        p = [np.zeros(L, np.uint8) for _ in range(m)]
+        hs = RSCoder(k, m).encode_hashed_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L)
+        want = oracle.Encoder(k, m).encode(d) if L else [np.zeros(0, np.uint8)] * m
+        for r in range(m):
+            assert np.array_equal(p[r], want[r])
+            assert hs[r] == java_bytebuffer_hash(want[r])

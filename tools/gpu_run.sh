@@ -38,7 +38,9 @@ for step in "$@"; do
     configs)
         run bench_mixed 400 python bench.py --config mixed || exit $?
         run bench_rs12 400 python bench.py --config rs12 || exit $?
-        run bench_hostpath 400 python bench.py --config hostpath || exit $? ;;
+        run bench_hostpath 400 python bench.py --config hostpath || exit $?
+        run bench_update 400 python bench.py --config update || exit $?
+        run bench_padded 400 python bench.py --config padded || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
