@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (PCIe) measurement")
     ap.add_argument("--config", default="headline",
-                    choices=["headline", "mixed", "rs12", "hostpath", "update", "padded"],
+                    choices=["headline", "mixed", "rs12", "hostpath", "update", "padded", "hashed"],
                     help="headline = the driver's line (BASELINE configs[1]+[2]); mixed = configs[3] "
                          "(1 KiB/4 KiB/1 MiB, 1 GiB per class over all ranks); rs12 = configs[4] "
                          "(RS(12,8) two-erasure decode, 256 KiB, 512 stripes per GPU); hostpath = the "
@@ -376,13 +376,55 @@ def config_padded(args, world, rank, dev):
                        "parallelism": f"stripe-partitioned x{world}"}}
 
 
+def config_hashed(args, world, rank, dev):
+    """RS(6,4) encode with the fused parity hash
+    (java.nio.ByteBuffer.hashCode of every parity unit), 64 KiB, 4096 stripes."""
+    from elect_amd.batch import encode_batch, encode_batch_hashed
+    from elect_amd.coder import RSCoder
+    k, m, L, B = 4, 2, 65536, 4096
+    coder = RSCoder(k, m)
+    data = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev)
+    par = torch.empty((B, m, L), dtype=torch.uint8, device=dev)
+    hashes = torch.empty((B, m), dtype=torch.int32, device=dev)
+    evs = []
+
+    def step():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        encode_batch_hashed(coder, data, par, hashes)
+        e1.record()
+        evs.append((e0, e1))
+
+    dt = timed(step, args.steps, args.warmup, world)
+    ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
+    ref = torch.empty_like(par)
+    encode_batch(coder, data, ref)
+    # spot-check two hashes against the closed form on the host
+    from elect_amd.coder import java_bytebuffer_hash
+    h = hashes.cpu()
+    ok = torch.equal(par, ref) and all(int(h[s, r]) == java_bytebuffer_hash(par[s, r].cpu().numpy())
+                                       for s, r in ((0, 0), (B - 1, m - 1)))
+    alg = B * (k + m) * L
+    gbs = alg / (ms * 1e-3) / 1e9
+    return {"metric": "GiB/s device-resident RS(6,4) encode + fused parity hashCode, 64 KiB chunks",
+            "value": round(world * args.steps * B * k * L / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic", "verified": ok,
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "gf_apply_x16<4,2> + hash epilogue", "algorithmic_bytes_per_launch": alg},
+            "config": {"workload": f"{B} x {L} B stripes per GPU, hashes [B, m] int32",
+                       "parallelism": f"stripe-partitioned x{world}"}}
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
     if args.config != "headline":
         dev = torch.device("cuda", local if world > 1 else 0)
         fn = {"mixed": config_mixed, "rs12": config_rs12, "hostpath": config_hostpath,
-              "update": config_update, "padded": config_padded}[args.config]
+              "update": config_update, "padded": config_padded, "hashed": config_hashed}[args.config]
         out = fn(args, world, rank, dev)
         if rank == 0:
             print(json.dumps(out), flush=True)

@@ -40,7 +40,8 @@ for step in "$@"; do
         run bench_rs12 400 python bench.py --config rs12 || exit $?
         run bench_hostpath 400 python bench.py --config hostpath || exit $?
         run bench_update 400 python bench.py --config update || exit $?
-        run bench_padded 400 python bench.py --config padded || exit $? ;;
+        run bench_padded 400 python bench.py --config padded || exit $?
+        run bench_hashed 400 python bench.py --config hashed || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
