@@ -148,19 +148,38 @@ __device__ __forceinline__ uint32_t dpow31(uint64_t e)
     return r;
 }
 
-// sum_t sb[t] * 31^t over the 16 bytes of a segment (Horner from the top byte).
+// sum_t sb[t] * 31^t over the 16 bytes of a segment.  v_dot4_i32_i8 reads the
+// bytes as signed int8, which is Java's byte: per dword D = (b0 + 31 b1) +
+// 961 (b2 + 31 b3), then a Horner step of 31^4 per dword.
 __device__ __forceinline__ uint32_t horner31(const uint4& v)
 {
     uint32_t h = 0;
 #pragma unroll
     for (int w = 3; w >= 0; --w) {
-        const uint32_t x = lane_word(v, w);
-#pragma unroll
-        for (int b = 3; b >= 0; --b)
-            h = h * 31u + static_cast<uint32_t>(static_cast<int32_t>(x << (24 - 8 * b)) >> 24);
+        const int x = static_cast<int>(lane_word(v, w));
+        const int lo = __builtin_amdgcn_sdot4(x, 0x00001F01, 0, false);
+        const int hi = __builtin_amdgcn_sdot4(x, 0x1F010000, 0, false);
+        const uint32_t d = static_cast<uint32_t>(__mul24(hi, 961) + lo);
+        h = w == 3 ? d : h * 923521u + d;  // 923521 = 31^4
     }
     return h;
 }
+
+// 31^(16*lane) for lane 0..63, a compile-time table (constant memory).
+struct LanePow {
+    uint32_t v[64];
+    constexpr LanePow() : v()
+    {
+        uint32_t p16 = 1;
+        for (int i = 0; i < 16; ++i) p16 *= 31u;
+        uint32_t x = 1;
+        for (int l = 0; l < 64; ++l) {
+            v[l] = x;
+            x *= p16;
+        }
+    }
+};
+__constant__ constexpr LanePow kLanePow{};
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 {
@@ -219,16 +238,33 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
     const uint64_t off = static_cast<uint64_t>(idx - stripe * a.segs) * 16;
 
     uint4 x[K];
+    if (!PAD) {
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-        const uint8_t* p = a.sp[j] + stripe * a.ss[j] + off;
-        if (!PAD) {
-            x[j] = load_nt(p);
+        for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + stripe * a.ss[j] + off);
+    } else {
+        // Full segments first (no loads at all past a column's content length),
+        // then the rare straddling segment into separate registers, so no load
+        // waits on another.
+        uint32_t valid[K];
+        if (a.lens) {  // all lengths first: vmcnt is in order, so interleaving would serialise
+            const uint32_t* l = a.lens + static_cast<uint64_t>(stripe) * a.lstride;
+#pragma unroll
+            for (int j = 0; j < K; ++j) valid[j] = l[j];
         } else {
-            const uint64_t valid = a.lens ? a.lens[static_cast<uint64_t>(stripe) * a.lstride + j] : a.clen[j];
-            if (off + 16 <= valid) x[j] = load_nt(p);
-            else if (off >= valid) x[j] = make_uint4(0, 0, 0, 0);
-            else x[j] = load_partial(p, static_cast<uint32_t>(valid - off));
+#pragma unroll
+            for (int j = 0; j < K; ++j) valid[j] = a.clen[j];
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            x[j] = make_uint4(0, 0, 0, 0);
+            if (off + 16 <= valid[j]) x[j] = load_nt(a.sp[j] + stripe * a.ss[j] + off);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            if (off < valid[j] && off + 16 > valid[j]) {
+                const uint4 t = load_partial(a.sp[j] + stripe * a.ss[j] + off, static_cast<uint32_t>(valid[j] - off));
+                x[j] = make_uint4(x[j].x | t.x, x[j].y | t.y, x[j].z | t.z, x[j].w | t.w);
+            }
         }
     }
 
@@ -286,10 +322,10 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         if (whole_wave) {
             const uint32_t seg0 = first - s_first * a.segs;
             const uint32_t p0 = dpow31(a.hbase + static_cast<uint64_t>(seg0) * 16);
-            const uint32_t pl = dpow31(16u * (threadIdx.x & 63u));
+            const uint32_t q = kLanePow.v[threadIdx.x & 63u] * p0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const uint32_t sum = wave_sum(horner31(acc[r]) * pl * p0);
+                const uint32_t sum = wave_sum(horner31(acc[r]) * q);
                 if ((threadIdx.x & 63u) == 0)
                     atomicAdd(reinterpret_cast<unsigned*>(a.hashes) + static_cast<uint64_t>(stripe) * a.hstride + r, sum);
             }

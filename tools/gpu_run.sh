@@ -5,6 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
+rm -f gpurun_out/*.log gpurun_out/status.txt  # no stale logs from an earlier call
 export PYTHONUNBUFFERED=1
 export TMPDIR=/tmp
 OUT="$PWD/gpurun_out"
