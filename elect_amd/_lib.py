@@ -67,6 +67,7 @@ SIGNATURES = [
     ("elect_ec_version", ctypes.c_char_p, []),
     ("elect_ec_strerror", ctypes.c_char_p, [ctypes.c_int]),
     ("elect_ec_device_count", ctypes.c_int, [_ip]),
+    ("elect_ec_set_host_devices", ctypes.c_int, [_ip, ctypes.c_int]),
     ("elect_ec_coder_create", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_cp)]),
     ("elect_ec_coder_destroy", None, [_cp]),
     ("elect_ec_coder_num_data_units", ctypes.c_int, [_cp]),
@@ -128,6 +129,13 @@ def device_count() -> int:
     n = ctypes.c_int(0)
     lib.elect_ec_device_count(ctypes.byref(n))
     return n.value
+
+
+def set_host_devices(devices) -> None:
+    """Spread host-memory calls of different threads over these devices (round robin)."""
+    devices = list(devices)
+    check(lib.elect_ec_set_host_devices(int_array(devices) if devices else None, len(devices)),
+          "set_host_devices")
 
 
 def ptr_array(addrs) -> ctypes.Array:

@@ -12,10 +12,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <new>
+#include <string>
+#include <vector>
 
 #include "gf256.hpp"
 #include "rs_kernels.hpp"
@@ -295,6 +299,69 @@ private:
 constexpr int kMaxDevices = 64;
 thread_local std::unique_ptr<HostEngine> t_engines[kMaxDevices];
 
+// Device policy of the host-memory path (elect_ec_set_host_devices).
+struct DevicePolicy {
+    std::mutex mu;
+    bool env_read = false;
+    std::vector<int> devices;  // empty: each thread's current device
+    std::atomic<unsigned> next{0};
+    std::atomic<unsigned> generation{1};
+};
+
+DevicePolicy& policy()
+{
+    static DevicePolicy p;
+    return p;
+}
+
+int parse_device_env(int ndev, std::vector<int>& out)
+{
+    const char* env = std::getenv("ELECT_EC_DEVICES");
+    out.clear();
+    if (!env || !*env) return ELECT_EC_OK;
+    const std::string v(env);
+    if (v == "all") {
+        for (int d = 0; d < ndev; ++d) out.push_back(d);
+        return ELECT_EC_OK;
+    }
+    size_t i = 0;
+    while (i < v.size()) {
+        size_t j = v.find(',', i);
+        if (j == std::string::npos) j = v.size();
+        const int d = std::atoi(v.substr(i, j - i).c_str());
+        if (d < 0 || d >= ndev) return ELECT_EC_EINVAL;
+        out.push_back(d);
+        i = j + 1;
+    }
+    return ELECT_EC_OK;
+}
+
+thread_local int t_device = -1;
+thread_local unsigned t_generation = 0;
+
+// The device this thread's host-memory calls run on.
+int host_device(int ndev, int* dev)
+{
+    DevicePolicy& p = policy();
+    {
+        std::lock_guard<std::mutex> lock(p.mu);
+        if (!p.env_read) {
+            p.env_read = true;
+            if (p.devices.empty() && parse_device_env(ndev, p.devices) != ELECT_EC_OK) p.devices.clear();
+        }
+        if (p.devices.empty()) {
+            const hipError_t e = hipGetDevice(dev);
+            return map_hip(e);
+        }
+        if (t_device < 0 || t_generation != p.generation.load()) {
+            t_device = p.devices[p.next++ % p.devices.size()];
+            t_generation = p.generation.load();
+        }
+    }
+    *dev = t_device;
+    return ELECT_EC_OK;
+}
+
 int run_host(const HostOp& op, size_t len)
 {
     if (len == 0) return ELECT_EC_OK;  // JEC/ErasureEncoder.java:41-44, JEC/ErasureDecoder.java:36-38
@@ -307,14 +374,20 @@ int run_host(const HostOp& op, size_t len)
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return ELECT_EC_ENODEV;
     int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
+    int rc = host_device(ndev, &dev);
+    if (rc != ELECT_EC_OK) return rc;
+    if (dev < 0 || dev >= kMaxDevices || dev >= ndev) return ELECT_EC_ENODEV;
+    int prev = 0;
+    hipError_t e = hipGetDevice(&prev);
+    if (e == hipSuccess && prev != dev) e = hipSetDevice(dev);
     if (e != hipSuccess) return map_hip(e);
-    if (dev < 0 || dev >= kMaxDevices) return ELECT_EC_ENODEV;
     if (!t_engines[dev]) {
         t_engines[dev].reset(new (std::nothrow) HostEngine(dev));
-        if (!t_engines[dev]) return ELECT_EC_ENOMEM;
+        if (!t_engines[dev]) rc = ELECT_EC_ENOMEM;
     }
-    return t_engines[dev]->run(op, len);
+    if (rc == ELECT_EC_OK) rc = t_engines[dev]->run(op, len);
+    if (prev != dev) (void)hipSetDevice(prev);  // the caller's current device is left as it was
+    return rc;
 }
 
 bool valid_coder(const elect_ec_coder* c) { return c && c->k >= 1 && c->m >= 1; }
@@ -346,6 +419,22 @@ int elect_ec_device_count(int* count)
     const hipError_t e = hipGetDeviceCount(&n);
     *count = e == hipSuccess ? n : 0;
     return (e == hipSuccess && n > 0) ? ELECT_EC_OK : ELECT_EC_ENODEV;
+}
+
+int elect_ec_set_host_devices(const int* devices, int n)
+{
+    if (n < 0 || (n > 0 && !devices)) return ELECT_EC_EINVAL;
+    int ndev = 0;
+    if (n > 0 && (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)) return ELECT_EC_ENODEV;
+    for (int i = 0; i < n; ++i)
+        if (devices[i] < 0 || devices[i] >= ndev || devices[i] >= kMaxDevices) return ELECT_EC_EINVAL;
+    DevicePolicy& p = policy();
+    std::lock_guard<std::mutex> lock(p.mu);
+    p.env_read = true;  // an explicit list overrides the environment
+    p.devices.assign(devices, devices + n);
+    p.next = 0;
+    p.generation++;  // threads pick a device again on their next call
+    return ELECT_EC_OK;
 }
 
 int elect_ec_coder_create(int num_data_units, int num_parity_units, elect_ec_coder** out)

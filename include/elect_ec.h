@@ -75,6 +75,15 @@ const char* elect_ec_strerror(int status);
 /* Number of visible HIP devices (0 with ELECT_EC_ENODEV when none). */
 int elect_ec_device_count(int* count);
 
+/* Devices for the host-memory calls.  By default a calling thread uses its
+ * current HIP device.  With a device list, each calling thread is assigned one
+ * device of the list (round robin, on its first call) and keeps it, so one
+ * process — ELECT runs one JVM per node — spreads its coding threads over every
+ * GPU of the node.  The list can also come from the environment:
+ * ELECT_EC_DEVICES=all or ELECT_EC_DEVICES=0,2,5 (read once, at the first call).
+ * n = 0 restores the default.  Returns ELECT_EC_EINVAL for an unknown device. */
+int elect_ec_set_host_devices(const int* devices, int n);
+
 /* ---- coder lifecycle ----
  * Replaces initEncoder / initDecoder (EC/erasure_coder.c:49-72) as called by
  * NativeRSEncoder_initImpl (EC/NativeRSEncoder.c:31-40) and NativeRSDecoder_initImpl

@@ -391,3 +391,36 @@ def test_encode_hashed_host_path(dev, oracle):
         for r in range(m):
             assert np.array_equal(p[r], want[r])
             assert hs[r] == java_bytebuffer_hash(want[r])
+
+
+def test_host_device_policy(dev, oracle):
+    """elect_ec_set_host_devices: threads pinned round robin to the listed devices
+    (one JVM driving every GPU of a node); bad ids rejected; default restored."""
+    import threading
+    from elect_amd import _lib
+    from elect_amd.coder import RSCoder
+    ndev = torch.cuda.device_count()
+    with pytest.raises(_lib.ECInvalidArgument):
+        _lib.set_host_devices([ndev])
+    _lib.set_host_devices(list(range(ndev)))
+    try:
+        k, m, L = 4, 2, 70001
+        coder = RSCoder(k, m)
+        ok = []
+
+        def worker(t):
+            rng = np.random.default_rng(t)
+            d = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+            p = [np.empty(L, np.uint8) for _ in range(m)]
+            coder.encode_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L)
+            want = oracle.Encoder(k, m).encode(d)
+            ok.append(all(np.array_equal(a, b) for a, b in zip(p, want)))
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(2 * ndev + 1)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert ok and all(ok)
+    finally:
+        _lib.set_host_devices([])
