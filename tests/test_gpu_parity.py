@@ -424,3 +424,64 @@ def test_host_device_policy(dev, oracle):
         assert ok and all(ok)
     finally:
         _lib.set_host_devices([])
+
+
+def test_launch_split_beyond_2pow31_segments(dev):
+    """A batch with more than 2^31 16-byte segments is split into several launches
+    (per-launch index < 2^31).  RS(2,1) has E[1][0] = 1/(1^0) = 1, so its parity
+    must equal the data exactly: a size-independent check at 32 GiB per column."""
+    from elect_amd.batch import encode_batch
+    from elect_amd.coder import RSCoder
+    free, _ = torch.cuda.mem_get_info()
+    B, L = (1 << 31) + 4099, 16
+    if free < 2 * B * L + (4 << 30):
+        pytest.skip("needs ~70 GiB of free HBM")
+    data = torch.empty((B, 1, L), dtype=torch.uint8, device=dev)
+    data.view(-1)[: 1 << 20].random_(0, 256)
+    data.view(-1)[-(1 << 20):].random_(0, 256)
+    par = torch.zeros((B, 1, L), dtype=torch.uint8, device=dev)
+    encode_batch(RSCoder(1, 1), data, par)
+    torch.cuda.synchronize()
+    assert torch.equal(par.view(-1)[: 1 << 20], data.view(-1)[: 1 << 20])
+    assert torch.equal(par.view(-1)[-(1 << 20):], data.view(-1)[-(1 << 20):])  # last launch window
+    del data, par
+    torch.cuda.empty_cache()
+
+
+def test_rs12_8_every_double_erasure_at_256k(dev):
+    """BASELINE configs[4] shape: RS(12,8), 256 KiB chunks; every 2-erasure
+    pattern (66) rebuilt in strict mode from the first 8 survivors must equal the
+    lost units (MDS round trip at full size)."""
+    from elect_amd.batch import decode_batch, encode_batch
+    from elect_amd.coder import RSCoder
+    k, m, L, B = 8, 4, 262144, 32
+    c = RSCoder(k, m)
+    st = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
+    st[:, :k].random_(0, 256)
+    encode_batch(c, st[:, :k], st[:, k:])
+    out = torch.empty((B, 2, L), dtype=torch.uint8, device=dev)
+    for erased in itertools.combinations(range(k + m), 2):
+        surv = [i for i in range(k + m) if i not in erased][:k]
+        decode_batch(c, st, surv, list(erased), out, mode=1, inputs_by_unit=True)
+        assert torch.equal(out[:, 0], st[:, erased[0]]) and torch.equal(out[:, 1], st[:, erased[1]]), erased
+
+
+def test_mixed_size_batch_properties(dev, oracle):
+    """BASELINE configs[3] shape, scaled: 1 KiB / 4 KiB / 1 MiB classes; sampled
+    stripes against the oracle, every stripe by the decode round trip."""
+    from elect_amd.batch import decode_batch, encode_batch
+    from elect_amd.coder import RSCoder
+    k, m = 4, 2
+    c = RSCoder(k, m)
+    enc = oracle.Encoder(k, m)
+    for L, B in ((1024, 8192), (4096, 2048), (1 << 20, 16)):
+        st = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
+        st[:, :k].random_(0, 256)
+        encode_batch(c, st[:, :k], st[:, k:])
+        out = torch.empty((B, 1, L), dtype=torch.uint8, device=dev)
+        decode_batch(c, st, [1, 2, 3, 4], [0], out, inputs_by_unit=True)
+        assert torch.equal(out[:, 0], st[:, 0])
+        for s in (0, B // 2, B - 1):
+            h = st[s].cpu().numpy()
+            want = enc.encode([h[j] for j in range(k)])
+            assert np.array_equal(h[k], want[0]) and np.array_equal(h[k + 1], want[1])
