@@ -103,3 +103,11 @@ def test_java_hash_closed_form_equals_jdk_loop():
             h = (31 * h + int(x)) & 0xFFFFFFFF
         h = h - (1 << 32) if h >= 1 << 31 else h
         assert java_bytebuffer_hash(b) == h
+
+
+def test_cpp_mirror_error_behaviour():
+    """include/elect_ec.hpp (C++ mirror of the Java API): same checks and exceptions."""
+    import subprocess
+    from tests.cpp_build import build
+    r = subprocess.run([build(), "cpu"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr

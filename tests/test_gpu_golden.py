@@ -112,3 +112,17 @@ def test_golden_erasure_code_test_port_on_gpu(dev):
     assert out2[0].compareTo(modified[0].rewind()) == 0      # :119
     enc.release()
     dec.release()
+
+
+def test_cpp_mirror_erasure_code_test_on_gpu(dev, tmp_path):
+    """ErasureCodeTest.java through the C++ mirror (include/elect_ec.hpp) on the GPU."""
+    import subprocess
+    from tests.cpp_build import build
+    r = subprocess.run([build(), "gpu", str(tmp_path)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    g = load("erasure_code_test.json")
+    rd = lambda n: np.fromfile(tmp_path / n, dtype=np.uint8)  # noqa: E731
+    assert [digest(rd(f"data{i}")) for i in range(4)] == g["data"]
+    assert [digest(rd(f"parity{r}")) for r in range(2)] == g["parity"]
+    assert [digest(rd(f"second{r}")) for r in range(2)] == g["second_parity"]
+    assert [digest(rd(f"update{r}")) for r in range(2)] == g["update_parity"]
