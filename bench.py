@@ -54,6 +54,8 @@ def parse():
                          "(RS(12,8) two-erasure decode, 256 KiB, 512 stripes per GPU); hostpath = the "
                          "JNI-style synchronous host-memory encode at ELECT's codeLength")
     ap.add_argument("--threads", type=int, default=16, help="hostpath: concurrent callers")
+    ap.add_argument("--batch", action="store_true", help="hostpath: cross-thread batching on")
+    ap.add_argument("--host-chunk", type=int, default=4404020, help="hostpath: bytes per unit per call")
     return ap.parse_args()
 
 
@@ -251,15 +253,17 @@ def config_hostpath(args, world, rank, dev):
     import numpy as np
 
     from elect_amd.coder import RSCoder
-    k, m, L = 4, 2, 4404020
+    from elect_amd import _lib
+    k, m, L = 4, 2, args.host_chunk
     T = args.threads
     coder = RSCoder(k, m)
+    _lib.set_batching(args.batch)
     bufs = []
     for t in range(T):
         d = [np.random.default_rng(t * 8 + j).integers(0, 256, L, dtype=np.uint8) for j in range(k)]
         p = [np.empty(L, np.uint8) for _ in range(m)]
         bufs.append((d, p))
-    calls = max(4, args.steps // 2)
+    calls = max(4, args.steps // 2) * max(1, 4404020 // L // 8)
 
     def worker(t, n):
         torch.cuda.set_device(dev)
@@ -290,7 +294,8 @@ def config_hostpath(args, world, rank, dev):
             "scaling": "none", "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
             "config": {"workload": f"{T} threads x {calls} synchronous elect_ec_encode calls, one stripe "
                                    f"of {k} x {L} B each, pageable host buffers",
-                       "parallelism": "per-thread pinned staging + 2 streams"}}
+                       "parallelism": "cross-thread batching (shared pinned arena, one launch per batch)"
+                                      if args.batch else "per-thread pinned staging + 2 streams"}}
 
 
 def config_update(args, world, rank, dev):

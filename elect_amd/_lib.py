@@ -68,6 +68,7 @@ SIGNATURES = [
     ("elect_ec_strerror", ctypes.c_char_p, [ctypes.c_int]),
     ("elect_ec_device_count", ctypes.c_int, [_ip]),
     ("elect_ec_set_host_devices", ctypes.c_int, [_ip, ctypes.c_int]),
+    ("elect_ec_set_batching", ctypes.c_int, [ctypes.c_int, ctypes.c_uint, ctypes.c_size_t]),
     ("elect_ec_coder_create", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_cp)]),
     ("elect_ec_coder_destroy", None, [_cp]),
     ("elect_ec_coder_num_data_units", ctypes.c_int, [_cp]),
@@ -136,6 +137,11 @@ def set_host_devices(devices) -> None:
     devices = list(devices)
     check(lib.elect_ec_set_host_devices(int_array(devices) if devices else None, len(devices)),
           "set_host_devices")
+
+
+def set_batching(enable: bool, window_us: int = 500, arena_bytes: int = 256 << 20) -> None:
+    """Cross-thread batching of concurrent host-memory encodes/decodes of one shape."""
+    check(lib.elect_ec_set_batching(int(enable), window_us, arena_bytes), "set_batching")
 
 
 def ptr_array(addrs) -> ctypes.Array:

@@ -15,8 +15,8 @@ BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libelect_ec.so")
 ARCH = os.environ.get("ELECT_EC_ARCH", "gfx950")
 
-SOURCES = ["ec_capi.cpp", "rs_kernels.hip"]
-HEADERS = ["gf256.hpp", "rs_kernels.hpp"]
+SOURCES = ["ec_capi.cpp", "host_path.cpp", "rs_kernels.hip"]
+HEADERS = ["gf256.hpp", "rs_kernels.hpp", "host_path.hpp"]
 
 
 def _hipcc() -> str:

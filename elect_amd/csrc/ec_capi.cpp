@@ -12,16 +12,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
-#include <cstdlib>
 #include <cstring>
-#include <memory>
-#include <mutex>
 #include <new>
-#include <string>
-#include <vector>
 
 #include "gf256.hpp"
+#include "host_path.hpp"
 #include "rs_kernels.hpp"
 
 struct elect_ec_coder {
@@ -34,22 +29,13 @@ struct elect_ec_coder {
 
 namespace {
 
+using elect::host::col;
+using elect::host::HostOp;
+using elect::host::map_hip;
+using elect::host::run_host;
 using elect::kern::ApplyParams;
 using elect::kern::Column;
 using elect::kern::UpdateParams;
-
-int map_hip(hipError_t e)
-{
-    switch (e) {
-    case hipSuccess: return ELECT_EC_OK;
-    case hipErrorNoDevice:
-    case hipErrorInvalidDevice:
-    case hipErrorNoBinaryForGpu: return ELECT_EC_ENODEV;
-    case hipErrorOutOfMemory: return ELECT_EC_ENOMEM;
-    case hipErrorInvalidValue: return ELECT_EC_EINVAL;
-    default: return ELECT_EC_EDEVICE;
-    }
-}
 
 const uint8_t* parity_row(const elect_ec_coder* c, int r) { return c->gen + (c->k + r) * c->k; }
 
@@ -101,295 +87,6 @@ int build_decode_matrix(const elect_ec_coder* c, const int* decode_indexes, cons
 
 hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
 
-Column col(const void* base, size_t stripe_stride, size_t offset)
-{
-    Column c;
-    c.ptr = static_cast<const uint8_t*>(base) + offset;
-    c.stride = stripe_stride;
-    return c;
-}
-
-// ---------------------------------------------------------------------------
-// Host-memory path: per-thread, per-device staging engine.
-// Input chunks are copied into pinned buffers, sent H2D, coded, returned D2H
-// and copied out, with two slots (streams) so chunk c+1's transfers overlap
-// chunk c's kernel and host copies.
-// ---------------------------------------------------------------------------
-struct HostOp {
-    int cols = 0;
-    int rows = 0;
-    bool update = false;  // cols = 2 + rows: [old, new, P...]; else an apply
-    const unsigned char* const* in = nullptr;
-    unsigned char* const* out = nullptr;
-    uint8_t coef[elect::kern::kMaxRows * elect::kern::kMaxCols] = {};
-    const size_t* lens = nullptr;  // optional content length per input (implicit zero padding)
-    int32_t* hashes = nullptr;     // optional host output: ByteBuffer.hashCode() per output row
-};
-
-class HostEngine {
-public:
-    static constexpr size_t kChunk = size_t{1} << 20;  // bytes per shard per pipeline step
-    static constexpr int kSlots = 2;
-
-    explicit HostEngine(int dev) : dev_(dev) {}
-    ~HostEngine()
-    {
-        for (int s = 0; s < kSlots; ++s) {
-            if (stream_[s]) (void)hipStreamDestroy(stream_[s]);
-            if (pin_in_[s]) (void)hipHostFree(pin_in_[s]);
-            if (pin_out_[s]) (void)hipHostFree(pin_out_[s]);
-            if (d_in_[s]) (void)hipFree(d_in_[s]);
-            if (d_out_[s]) (void)hipFree(d_out_[s]);
-        }
-        if (d_hash_) (void)hipFree(d_hash_);
-    }
-
-    int run(const HostOp& op, size_t len)
-    {
-        const size_t step = std::min(len, kChunk);
-        const size_t pitch = (step + 255) & ~size_t{255};
-        int rc = reserve(static_cast<size_t>(op.cols) * pitch, static_cast<size_t>(op.rows) * pitch);
-        if (rc != ELECT_EC_OK) return rc;
-        const size_t nchunks = (len + step - 1) / step;
-        if (op.hashes) {  // every chunk's kernel adds into d_hash_; start from 31^len
-            hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_hash_),
-                                             static_cast<int>(elect::kern::pow31(len)), op.rows, stream_[0]);
-            if (e == hipSuccess) e = hipStreamSynchronize(stream_[0]);
-            if (e != hipSuccess) return map_hip(e);
-        }
-        size_t pending[kSlots] = {};
-        bool busy[kSlots] = {};
-        for (size_t c = 0; c < nchunks + kSlots; ++c) {
-            const int s = static_cast<int>(c % kSlots);
-            if (busy[s]) {  // retire the chunk that used this slot
-                const hipError_t e = hipStreamSynchronize(stream_[s]);
-                if (e != hipSuccess) return map_hip(e);
-                const size_t o = pending[s] * step;
-                const size_t n = std::min(step, len - o);
-                for (int r = 0; r < op.rows; ++r) std::memcpy(op.out[r] + o, pin_out_[s] + r * pitch, n);
-                busy[s] = false;
-            }
-            if (c >= nchunks) continue;
-            const size_t o = c * step;
-            const size_t n = std::min(step, len - o);
-            hipError_t e = hipSuccess;
-            uint32_t valid[elect::kern::kMaxCols];
-            if (op.lens) {  // copy and send only each column's valid bytes
-                for (int j = 0; j < op.cols && e == hipSuccess; ++j) {
-                    const size_t v = op.lens[j] > o ? std::min(n, op.lens[j] - o) : 0;
-                    valid[j] = static_cast<uint32_t>(v);
-                    if (v == 0) continue;
-                    std::memcpy(pin_in_[s] + j * pitch, op.in[j] + o, v);
-                    e = hipMemcpyAsync(d_in_[s] + j * pitch, pin_in_[s] + j * pitch, v, hipMemcpyHostToDevice,
-                                       stream_[s]);
-                }
-            } else {
-                for (int j = 0; j < op.cols; ++j) std::memcpy(pin_in_[s] + j * pitch, op.in[j] + o, n);
-                e = hipMemcpyAsync(d_in_[s], pin_in_[s], op.cols * pitch, hipMemcpyHostToDevice, stream_[s]);
-            }
-            if (e == hipSuccess) e = launch(op, s, pitch, n, op.lens ? valid : nullptr, o);
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(pin_out_[s], d_out_[s], op.rows * pitch, hipMemcpyDeviceToHost, stream_[s]);
-            if (e != hipSuccess) {
-                (void)hipStreamSynchronize(stream_[0]);
-                (void)hipStreamSynchronize(stream_[1]);
-                return map_hip(e);
-            }
-            pending[s] = c;
-            busy[s] = true;
-        }
-        if (op.hashes) {
-            const hipError_t e = hipMemcpy(op.hashes, d_hash_, op.rows * sizeof(int32_t), hipMemcpyDeviceToHost);
-            if (e != hipSuccess) return map_hip(e);
-        }
-        return ELECT_EC_OK;
-    }
-
-private:
-    hipError_t launch(const HostOp& op, int s, size_t pitch, size_t n, const uint32_t* valid, size_t offset)
-    {
-        if (op.update) {
-            UpdateParams p;
-            p.len = n;
-            p.stripes = 1;
-            p.rows = op.rows;
-            p.old_data = col(d_in_[s], pitch, 0);
-            p.new_data = col(d_in_[s], pitch, pitch);
-            for (int r = 0; r < op.rows; ++r) {
-                p.par_in[r] = col(d_in_[s], pitch, (2 + r) * pitch);
-                p.par_out[r] = col(d_out_[s], pitch, r * pitch);
-                p.coef[r] = op.coef[r];
-            }
-            return elect::kern::launch_update(p, stream_[s]);
-        }
-        ApplyParams p;
-        p.len = n;
-        p.stripes = 1;
-        p.cols = op.cols;
-        p.rows = op.rows;
-        for (int j = 0; j < op.cols; ++j) p.src[j] = col(d_in_[s], pitch, j * pitch);
-        for (int r = 0; r < op.rows; ++r) p.dst[r] = col(d_out_[s], pitch, r * pitch);
-        std::memcpy(p.coef, op.coef, sizeof(p.coef));
-        if (valid) {
-            p.padded = true;
-            for (int j = 0; j < op.cols; ++j) p.clen[j] = valid[j];
-        }
-        if (op.hashes) {
-            p.hashes = d_hash_;
-            p.hash_stride = static_cast<uint32_t>(op.rows);
-            p.hash_base = offset;
-        }
-        return elect::kern::launch_apply(p, stream_[s]);
-    }
-
-    int reserve(size_t in_bytes, size_t out_bytes)
-    {
-        if (!stream_[0]) {
-            for (int s = 0; s < kSlots; ++s) {
-                const hipError_t e = hipStreamCreateWithFlags(&stream_[s], hipStreamNonBlocking);
-                if (e != hipSuccess) return map_hip(e);
-            }
-            const hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_hash_), elect::kern::kMaxRows * sizeof(int32_t));
-            if (e != hipSuccess) return map_hip(e);
-        }
-        if (in_bytes > cap_in_) {
-            for (int s = 0; s < kSlots; ++s) {
-                if (pin_in_[s]) (void)hipHostFree(pin_in_[s]);
-                if (d_in_[s]) (void)hipFree(d_in_[s]);
-                pin_in_[s] = nullptr;
-                d_in_[s] = nullptr;
-                hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&pin_in_[s]), in_bytes, hipHostMallocDefault);
-                if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_in_[s]), in_bytes);
-                if (e != hipSuccess) {
-                    cap_in_ = 0;
-                    return map_hip(e);
-                }
-            }
-            cap_in_ = in_bytes;
-        }
-        if (out_bytes > cap_out_) {
-            for (int s = 0; s < kSlots; ++s) {
-                if (pin_out_[s]) (void)hipHostFree(pin_out_[s]);
-                if (d_out_[s]) (void)hipFree(d_out_[s]);
-                pin_out_[s] = nullptr;
-                d_out_[s] = nullptr;
-                hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&pin_out_[s]), out_bytes, hipHostMallocDefault);
-                if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_out_[s]), out_bytes);
-                if (e != hipSuccess) {
-                    cap_out_ = 0;
-                    return map_hip(e);
-                }
-            }
-            cap_out_ = out_bytes;
-        }
-        return ELECT_EC_OK;
-    }
-
-    int dev_;
-    hipStream_t stream_[kSlots] = {};
-    uint8_t* pin_in_[kSlots] = {};
-    uint8_t* pin_out_[kSlots] = {};
-    uint8_t* d_in_[kSlots] = {};
-    uint8_t* d_out_[kSlots] = {};
-    size_t cap_in_ = 0;
-    size_t cap_out_ = 0;
-    int32_t* d_hash_ = nullptr;
-};
-
-constexpr int kMaxDevices = 64;
-thread_local std::unique_ptr<HostEngine> t_engines[kMaxDevices];
-
-// Device policy of the host-memory path (elect_ec_set_host_devices).
-struct DevicePolicy {
-    std::mutex mu;
-    bool env_read = false;
-    std::vector<int> devices;  // empty: each thread's current device
-    std::atomic<unsigned> next{0};
-    std::atomic<unsigned> generation{1};
-};
-
-DevicePolicy& policy()
-{
-    static DevicePolicy p;
-    return p;
-}
-
-int parse_device_env(int ndev, std::vector<int>& out)
-{
-    const char* env = std::getenv("ELECT_EC_DEVICES");
-    out.clear();
-    if (!env || !*env) return ELECT_EC_OK;
-    const std::string v(env);
-    if (v == "all") {
-        for (int d = 0; d < ndev; ++d) out.push_back(d);
-        return ELECT_EC_OK;
-    }
-    size_t i = 0;
-    while (i < v.size()) {
-        size_t j = v.find(',', i);
-        if (j == std::string::npos) j = v.size();
-        const int d = std::atoi(v.substr(i, j - i).c_str());
-        if (d < 0 || d >= ndev) return ELECT_EC_EINVAL;
-        out.push_back(d);
-        i = j + 1;
-    }
-    return ELECT_EC_OK;
-}
-
-thread_local int t_device = -1;
-thread_local unsigned t_generation = 0;
-
-// The device this thread's host-memory calls run on.
-int host_device(int ndev, int* dev)
-{
-    DevicePolicy& p = policy();
-    {
-        std::lock_guard<std::mutex> lock(p.mu);
-        if (!p.env_read) {
-            p.env_read = true;
-            if (p.devices.empty() && parse_device_env(ndev, p.devices) != ELECT_EC_OK) p.devices.clear();
-        }
-        if (p.devices.empty()) {
-            const hipError_t e = hipGetDevice(dev);
-            return map_hip(e);
-        }
-        if (t_device < 0 || t_generation != p.generation.load()) {
-            t_device = p.devices[p.next++ % p.devices.size()];
-            t_generation = p.generation.load();
-        }
-    }
-    *dev = t_device;
-    return ELECT_EC_OK;
-}
-
-int run_host(const HostOp& op, size_t len)
-{
-    if (len == 0) return ELECT_EC_OK;  // JEC/ErasureEncoder.java:41-44, JEC/ErasureDecoder.java:36-38
-    for (int j = 0; j < op.cols; ++j) {
-        if (op.lens && op.lens[j] > len) return ELECT_EC_EINVAL;
-        if (!op.in[j] && !(op.lens && op.lens[j] == 0)) return ELECT_EC_EINVAL;
-    }
-    for (int r = 0; r < op.rows; ++r)
-        if (!op.out[r]) return ELECT_EC_EINVAL;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return ELECT_EC_ENODEV;
-    int dev = 0;
-    int rc = host_device(ndev, &dev);
-    if (rc != ELECT_EC_OK) return rc;
-    if (dev < 0 || dev >= kMaxDevices || dev >= ndev) return ELECT_EC_ENODEV;
-    int prev = 0;
-    hipError_t e = hipGetDevice(&prev);
-    if (e == hipSuccess && prev != dev) e = hipSetDevice(dev);
-    if (e != hipSuccess) return map_hip(e);
-    if (!t_engines[dev]) {
-        t_engines[dev].reset(new (std::nothrow) HostEngine(dev));
-        if (!t_engines[dev]) rc = ELECT_EC_ENOMEM;
-    }
-    if (rc == ELECT_EC_OK) rc = t_engines[dev]->run(op, len);
-    if (prev != dev) (void)hipSetDevice(prev);  // the caller's current device is left as it was
-    return rc;
-}
-
 bool valid_coder(const elect_ec_coder* c) { return c && c->k >= 1 && c->m >= 1; }
 
 }  // namespace
@@ -421,20 +118,11 @@ int elect_ec_device_count(int* count)
     return (e == hipSuccess && n > 0) ? ELECT_EC_OK : ELECT_EC_ENODEV;
 }
 
-int elect_ec_set_host_devices(const int* devices, int n)
+int elect_ec_set_host_devices(const int* devices, int n) { return elect::host::set_host_devices(devices, n); }
+
+int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes)
 {
-    if (n < 0 || (n > 0 && !devices)) return ELECT_EC_EINVAL;
-    int ndev = 0;
-    if (n > 0 && (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)) return ELECT_EC_ENODEV;
-    for (int i = 0; i < n; ++i)
-        if (devices[i] < 0 || devices[i] >= ndev || devices[i] >= kMaxDevices) return ELECT_EC_EINVAL;
-    DevicePolicy& p = policy();
-    std::lock_guard<std::mutex> lock(p.mu);
-    p.env_read = true;  // an explicit list overrides the environment
-    p.devices.assign(devices, devices + n);
-    p.next = 0;
-    p.generation++;  // threads pick a device again on their next call
-    return ELECT_EC_OK;
+    return elect::host::set_batching(enable, window_us, arena_bytes);
 }
 
 int elect_ec_coder_create(int num_data_units, int num_parity_units, elect_ec_coder** out)

@@ -1,0 +1,551 @@
+// host_path.cpp — host-memory path of the C ABI (include/elect_ec.h):
+// the JNI calling convention, one synchronous stripe per call
+// (EC/NativeRSEncoder.c:43-61 -> EC/erasure_coder.c:74-98).
+#include "host_path.hpp"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace elect {
+namespace host {
+namespace {
+
+using kern::ApplyParams;
+using kern::UpdateParams;
+
+// ---------------------------------------------------------------------------
+// Host-memory path: per-thread, per-device staging engine.
+// Input chunks are copied into pinned buffers, sent H2D, coded, returned D2H
+// and copied out, with two slots (streams) so chunk c+1's transfers overlap
+// chunk c's kernel and host copies.
+// ---------------------------------------------------------------------------
+class HostEngine {
+public:
+    static constexpr size_t kChunk = size_t{1} << 20;  // bytes per shard per pipeline step
+    static constexpr int kSlots = 2;
+
+    explicit HostEngine(int dev) : dev_(dev) {}
+    ~HostEngine()
+    {
+        for (int s = 0; s < kSlots; ++s) {
+            if (stream_[s]) (void)hipStreamDestroy(stream_[s]);
+            if (pin_in_[s]) (void)hipHostFree(pin_in_[s]);
+            if (pin_out_[s]) (void)hipHostFree(pin_out_[s]);
+            if (d_in_[s]) (void)hipFree(d_in_[s]);
+            if (d_out_[s]) (void)hipFree(d_out_[s]);
+        }
+        if (d_hash_) (void)hipFree(d_hash_);
+    }
+
+    int run(const HostOp& op, size_t len)
+    {
+        const size_t step = std::min(len, kChunk);
+        const size_t pitch = (step + 255) & ~size_t{255};
+        int rc = reserve(static_cast<size_t>(op.cols) * pitch, static_cast<size_t>(op.rows) * pitch);
+        if (rc != ELECT_EC_OK) return rc;
+        const size_t nchunks = (len + step - 1) / step;
+        if (op.hashes) {  // every chunk's kernel adds into d_hash_; start from 31^len
+            hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_hash_),
+                                             static_cast<int>(kern::pow31(len)), op.rows, stream_[0]);
+            if (e == hipSuccess) e = hipStreamSynchronize(stream_[0]);
+            if (e != hipSuccess) return map_hip(e);
+        }
+        size_t pending[kSlots] = {};
+        bool busy[kSlots] = {};
+        for (size_t c = 0; c < nchunks + kSlots; ++c) {
+            const int s = static_cast<int>(c % kSlots);
+            if (busy[s]) {  // retire the chunk that used this slot
+                const hipError_t e = hipStreamSynchronize(stream_[s]);
+                if (e != hipSuccess) return map_hip(e);
+                const size_t o = pending[s] * step;
+                const size_t n = std::min(step, len - o);
+                for (int r = 0; r < op.rows; ++r) std::memcpy(op.out[r] + o, pin_out_[s] + r * pitch, n);
+                busy[s] = false;
+            }
+            if (c >= nchunks) continue;
+            const size_t o = c * step;
+            const size_t n = std::min(step, len - o);
+            hipError_t e = hipSuccess;
+            uint32_t valid[kern::kMaxCols];
+            if (op.lens) {  // copy and send only each column's valid bytes
+                for (int j = 0; j < op.cols && e == hipSuccess; ++j) {
+                    const size_t v = op.lens[j] > o ? std::min(n, op.lens[j] - o) : 0;
+                    valid[j] = static_cast<uint32_t>(v);
+                    if (v == 0) continue;
+                    std::memcpy(pin_in_[s] + j * pitch, op.in[j] + o, v);
+                    e = hipMemcpyAsync(d_in_[s] + j * pitch, pin_in_[s] + j * pitch, v, hipMemcpyHostToDevice,
+                                       stream_[s]);
+                }
+            } else {
+                for (int j = 0; j < op.cols; ++j) std::memcpy(pin_in_[s] + j * pitch, op.in[j] + o, n);
+                e = hipMemcpyAsync(d_in_[s], pin_in_[s], op.cols * pitch, hipMemcpyHostToDevice, stream_[s]);
+            }
+            if (e == hipSuccess) e = launch(op, s, pitch, n, op.lens ? valid : nullptr, o);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(pin_out_[s], d_out_[s], op.rows * pitch, hipMemcpyDeviceToHost, stream_[s]);
+            if (e != hipSuccess) {
+                (void)hipStreamSynchronize(stream_[0]);
+                (void)hipStreamSynchronize(stream_[1]);
+                return map_hip(e);
+            }
+            pending[s] = c;
+            busy[s] = true;
+        }
+        if (op.hashes) {
+            const hipError_t e = hipMemcpy(op.hashes, d_hash_, op.rows * sizeof(int32_t), hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return map_hip(e);
+        }
+        return ELECT_EC_OK;
+    }
+
+private:
+    hipError_t launch(const HostOp& op, int s, size_t pitch, size_t n, const uint32_t* valid, size_t offset)
+    {
+        if (op.update) {
+            UpdateParams p;
+            p.len = n;
+            p.stripes = 1;
+            p.rows = op.rows;
+            p.old_data = col(d_in_[s], pitch, 0);
+            p.new_data = col(d_in_[s], pitch, pitch);
+            for (int r = 0; r < op.rows; ++r) {
+                p.par_in[r] = col(d_in_[s], pitch, (2 + r) * pitch);
+                p.par_out[r] = col(d_out_[s], pitch, r * pitch);
+                p.coef[r] = op.coef[r];
+            }
+            return kern::launch_update(p, stream_[s]);
+        }
+        ApplyParams p;
+        p.len = n;
+        p.stripes = 1;
+        p.cols = op.cols;
+        p.rows = op.rows;
+        for (int j = 0; j < op.cols; ++j) p.src[j] = col(d_in_[s], pitch, j * pitch);
+        for (int r = 0; r < op.rows; ++r) p.dst[r] = col(d_out_[s], pitch, r * pitch);
+        std::memcpy(p.coef, op.coef, sizeof(p.coef));
+        if (valid) {
+            p.padded = true;
+            for (int j = 0; j < op.cols; ++j) p.clen[j] = valid[j];
+        }
+        if (op.hashes) {
+            p.hashes = d_hash_;
+            p.hash_stride = static_cast<uint32_t>(op.rows);
+            p.hash_base = offset;
+        }
+        return kern::launch_apply(p, stream_[s]);
+    }
+
+    int reserve(size_t in_bytes, size_t out_bytes)
+    {
+        if (!stream_[0]) {
+            for (int s = 0; s < kSlots; ++s) {
+                const hipError_t e = hipStreamCreateWithFlags(&stream_[s], hipStreamNonBlocking);
+                if (e != hipSuccess) return map_hip(e);
+            }
+            const hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_hash_), kern::kMaxRows * sizeof(int32_t));
+            if (e != hipSuccess) return map_hip(e);
+        }
+        if (in_bytes > cap_in_) {
+            for (int s = 0; s < kSlots; ++s) {
+                if (pin_in_[s]) (void)hipHostFree(pin_in_[s]);
+                if (d_in_[s]) (void)hipFree(d_in_[s]);
+                pin_in_[s] = nullptr;
+                d_in_[s] = nullptr;
+                hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&pin_in_[s]), in_bytes, hipHostMallocDefault);
+                if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_in_[s]), in_bytes);
+                if (e != hipSuccess) {
+                    cap_in_ = 0;
+                    return map_hip(e);
+                }
+            }
+            cap_in_ = in_bytes;
+        }
+        if (out_bytes > cap_out_) {
+            for (int s = 0; s < kSlots; ++s) {
+                if (pin_out_[s]) (void)hipHostFree(pin_out_[s]);
+                if (d_out_[s]) (void)hipFree(d_out_[s]);
+                pin_out_[s] = nullptr;
+                d_out_[s] = nullptr;
+                hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&pin_out_[s]), out_bytes, hipHostMallocDefault);
+                if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_out_[s]), out_bytes);
+                if (e != hipSuccess) {
+                    cap_out_ = 0;
+                    return map_hip(e);
+                }
+            }
+            cap_out_ = out_bytes;
+        }
+        return ELECT_EC_OK;
+    }
+
+    int dev_;
+    hipStream_t stream_[kSlots] = {};
+    uint8_t* pin_in_[kSlots] = {};
+    uint8_t* pin_out_[kSlots] = {};
+    uint8_t* d_in_[kSlots] = {};
+    uint8_t* d_out_[kSlots] = {};
+    size_t cap_in_ = 0;
+    size_t cap_out_ = 0;
+    int32_t* d_hash_ = nullptr;
+};
+
+constexpr int kMaxDevices = 64;
+thread_local std::unique_ptr<HostEngine> t_engines[kMaxDevices];
+
+// Device policy of the host-memory path (elect_ec_set_host_devices).
+struct DevicePolicy {
+    std::mutex mu;
+    bool env_read = false;
+    std::vector<int> devices;  // empty: each thread's current device
+    std::atomic<unsigned> next{0};
+    std::atomic<unsigned> generation{1};
+};
+
+DevicePolicy& policy()
+{
+    static DevicePolicy p;
+    return p;
+}
+
+int parse_device_env(int ndev, std::vector<int>& out)
+{
+    const char* env = std::getenv("ELECT_EC_DEVICES");
+    out.clear();
+    if (!env || !*env) return ELECT_EC_OK;
+    const std::string v(env);
+    if (v == "all") {
+        for (int d = 0; d < ndev; ++d) out.push_back(d);
+        return ELECT_EC_OK;
+    }
+    size_t i = 0;
+    while (i < v.size()) {
+        size_t j = v.find(',', i);
+        if (j == std::string::npos) j = v.size();
+        const int d = std::atoi(v.substr(i, j - i).c_str());
+        if (d < 0 || d >= ndev) return ELECT_EC_EINVAL;
+        out.push_back(d);
+        i = j + 1;
+    }
+    return ELECT_EC_OK;
+}
+
+thread_local int t_device = -1;
+thread_local unsigned t_generation = 0;
+
+// The device this thread's host-memory calls run on.
+int host_device(int ndev, int* dev)
+{
+    DevicePolicy& p = policy();
+    {
+        std::lock_guard<std::mutex> lock(p.mu);
+        if (!p.env_read) {
+            p.env_read = true;
+            if (p.devices.empty() && parse_device_env(ndev, p.devices) != ELECT_EC_OK) p.devices.clear();
+        }
+        if (p.devices.empty()) {
+            const hipError_t e = hipGetDevice(dev);
+            return map_hip(e);
+        }
+        if (t_device < 0 || t_generation != p.generation.load()) {
+            t_device = p.devices[p.next++ % p.devices.size()];
+            t_generation = p.generation.load();
+        }
+    }
+    *dev = t_device;
+    return ELECT_EC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Cross-thread batching.  ELECT makes up to concurrent_ec
+// (64, conf/elect.yaml:598) synchronous one-stripe calls at once.  With
+// batching on, concurrent calls of the same shape (k, m, len, coefficients)
+// share a pinned arena: every caller copies its own inputs in (in parallel),
+// one dispatcher thread per device issues ONE H2D, ONE launch over all the
+// stripes ([slot][k][pitch] layout) and ONE D2H, then each caller copies its
+// outputs out.  Two arenas alternate, so one fills while the other is in flight.
+// ---------------------------------------------------------------------------
+struct BatchConfig {
+    std::atomic<int> enabled{-1};  // -1: read ELECT_EC_BATCH on first use
+    std::atomic<unsigned> window_us{500};
+    std::atomic<size_t> arena_bytes{size_t{256} << 20};
+};
+
+BatchConfig& batch_config()
+{
+    static BatchConfig c;
+    if (c.enabled.load() < 0) {
+        const char* e = std::getenv("ELECT_EC_BATCH");
+        const char* w = std::getenv("ELECT_EC_BATCH_WINDOW_US");
+        const char* a = std::getenv("ELECT_EC_BATCH_ARENA_MB");
+        if (w) c.window_us = static_cast<unsigned>(std::atoi(w));
+        if (a && std::atoi(a) > 0) c.arena_bytes = static_cast<size_t>(std::atoi(a)) << 20;
+        int expect = -1;
+        c.enabled.compare_exchange_strong(expect, (e && std::atoi(e) > 0) ? 1 : 0);
+    }
+    return c;
+}
+
+class Batcher {
+public:
+    static constexpr int kFallback = 1000;  // request does not fit: run it directly
+
+    explicit Batcher(int dev) : dev_(dev) {}
+
+    int submit(const HostOp& op, size_t len)
+    {
+        const BatchConfig& cfg = batch_config();
+        const size_t pitch = (len + 255) & ~size_t{255};
+        const size_t arena = cfg.arena_bytes.load();
+        if (static_cast<size_t>(op.cols) * pitch > arena) return kFallback;
+
+        std::unique_lock<std::mutex> lock(mu_);
+        if (!started_) {
+            std::thread(&Batcher::worker, this).detach();  // lives as long as the process
+            started_ = true;
+        }
+        Slab* slab = nullptr;
+        int slot = -1;
+        for (;;) {
+            for (Slab& s : slabs_)
+                if (s.state == Slab::kOpen && s.matches(op, len) && s.reserved < s.capacity) {
+                    slab = &s;
+                    break;
+                }
+            if (!slab) {
+                for (Slab& s : slabs_)  // a different shape or a full arena closes the open batch
+                    if (s.state == Slab::kOpen) s.state = Slab::kClosed;
+                for (Slab& s : slabs_)
+                    if (s.state == Slab::kFree) {
+                        const int rc = s.open(op, len, pitch, arena);
+                        if (rc != ELECT_EC_OK) return rc;
+                        slab = &s;
+                        break;
+                    }
+            }
+            if (slab) break;
+            cv_.notify_all();
+            cv_.wait(lock);
+        }
+        slot = slab->reserved++;
+        slab->readers++;
+        cv_.notify_all();
+        lock.unlock();
+
+        const size_t in_stride = static_cast<size_t>(slab->cols) * pitch;
+        for (int j = 0; j < op.cols; ++j) std::memcpy(slab->pin_in + slot * in_stride + j * pitch, op.in[j], len);
+
+        lock.lock();
+        slab->filled++;
+        cv_.notify_all();
+        cv_.wait(lock, [&] { return slab->state == Slab::kDone; });
+        const int status = slab->status;
+        lock.unlock();
+
+        if (status == ELECT_EC_OK) {
+            const size_t out_stride = static_cast<size_t>(slab->rows) * pitch;
+            for (int r = 0; r < op.rows; ++r)
+                std::memcpy(op.out[r], slab->pin_out + slot * out_stride + r * pitch, len);
+        }
+        lock.lock();
+        if (--slab->readers == 0) {
+            slab->state = Slab::kFree;
+            cv_.notify_all();
+        }
+        return status;
+    }
+
+private:
+    struct Slab {
+        enum State { kFree, kOpen, kClosed, kInFlight, kDone } state = kFree;
+        int cols = 0, rows = 0;
+        size_t len = 0, pitch = 0;
+        uint8_t coef[kern::kMaxRows * kern::kMaxCols] = {};
+        int capacity = 0, reserved = 0, filled = 0, readers = 0, status = ELECT_EC_OK;
+        std::chrono::steady_clock::time_point opened;
+        uint8_t *pin_in = nullptr, *pin_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+        size_t cap_in = 0, cap_out = 0;
+        hipStream_t stream = nullptr;
+
+        bool matches(const HostOp& op, size_t n) const
+        {
+            return op.cols == cols && op.rows == rows && n == len &&
+                   std::memcmp(op.coef, coef, sizeof(coef)) == 0;
+        }
+
+        int open(const HostOp& op, size_t n, size_t p, size_t arena)
+        {
+            cols = op.cols;
+            rows = op.rows;
+            len = n;
+            pitch = p;
+            std::memcpy(coef, op.coef, sizeof(coef));
+            capacity = static_cast<int>(arena / (static_cast<size_t>(cols) * pitch));
+            const size_t need_in = static_cast<size_t>(capacity) * cols * pitch;
+            const size_t need_out = static_cast<size_t>(capacity) * rows * pitch;
+            hipError_t e = hipSuccess;
+            if (!stream) e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+            if (e == hipSuccess && need_in > cap_in) {
+                if (pin_in) (void)hipHostFree(pin_in);
+                if (d_in) (void)hipFree(d_in);
+                pin_in = d_in = nullptr;
+                cap_in = 0;
+                e = hipHostMalloc(reinterpret_cast<void**>(&pin_in), need_in, hipHostMallocDefault);
+                if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_in), need_in);
+                if (e == hipSuccess) cap_in = need_in;
+            }
+            if (e == hipSuccess && need_out > cap_out) {
+                if (pin_out) (void)hipHostFree(pin_out);
+                if (d_out) (void)hipFree(d_out);
+                pin_out = d_out = nullptr;
+                cap_out = 0;
+                e = hipHostMalloc(reinterpret_cast<void**>(&pin_out), need_out, hipHostMallocDefault);
+                if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_out), need_out);
+                if (e == hipSuccess) cap_out = need_out;
+            }
+            if (e != hipSuccess) return map_hip(e);
+            reserved = filled = readers = 0;
+            status = ELECT_EC_OK;
+            opened = std::chrono::steady_clock::now();
+            state = kOpen;
+            return ELECT_EC_OK;
+        }
+    };
+
+    void worker()
+    {
+        (void)hipSetDevice(dev_);
+        std::unique_lock<std::mutex> lock(mu_);
+        for (;;) {
+            Slab* s = nullptr;
+            cv_.wait(lock, [&] {
+                s = nullptr;
+                for (Slab& x : slabs_)
+                    if ((x.state == Slab::kOpen || x.state == Slab::kClosed) && (!s || x.opened < s->opened)) s = &x;
+                return s != nullptr;
+            });
+            // collect for the window (or until the arena is full), then wait for every copy-in
+            const auto deadline = s->opened + std::chrono::microseconds(batch_config().window_us.load());
+            cv_.wait_until(lock, deadline, [&] { return s->state != Slab::kOpen || s->reserved >= s->capacity; });
+            s->state = Slab::kClosed;
+            cv_.wait(lock, [&] { return s->filled == s->reserved; });
+            s->state = Slab::kInFlight;
+            const int n = s->reserved;
+            lock.unlock();
+            const int rc = n > 0 ? code(*s, n) : ELECT_EC_OK;
+            lock.lock();
+            s->status = rc;
+            s->state = Slab::kDone;
+            if (s->readers == 0) s->state = Slab::kFree;
+            cv_.notify_all();
+        }
+    }
+
+    static int code(Slab& s, int n)
+    {
+        const size_t in_stride = static_cast<size_t>(s.cols) * s.pitch;
+        const size_t out_stride = static_cast<size_t>(s.rows) * s.pitch;
+        hipError_t e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
+        if (e == hipSuccess) {
+            ApplyParams p;
+            p.len = s.len;
+            p.stripes = static_cast<uint64_t>(n);
+            p.cols = s.cols;
+            p.rows = s.rows;
+            for (int j = 0; j < s.cols; ++j) p.src[j] = col(s.d_in, in_stride, j * s.pitch);
+            for (int r = 0; r < s.rows; ++r) p.dst[r] = col(s.d_out, out_stride, r * s.pitch);
+            std::memcpy(p.coef, s.coef, sizeof(p.coef));
+            e = kern::launch_apply(p, s.stream);
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(s.pin_out, s.d_out, n * out_stride, hipMemcpyDeviceToHost, s.stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+        return map_hip(e);
+    }
+
+    int dev_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    bool started_ = false;
+    Slab slabs_[2];
+};
+
+Batcher* batcher(int dev)
+{
+    static std::mutex mu;
+    static Batcher* all[kMaxDevices] = {};  // never destroyed: their threads live until exit
+    std::lock_guard<std::mutex> lock(mu);
+    if (!all[dev]) all[dev] = new (std::nothrow) Batcher(dev);
+    return all[dev];
+}
+
+}  // namespace
+
+int run_host(const HostOp& op, size_t len)
+{
+    if (len == 0) return ELECT_EC_OK;  // JEC/ErasureEncoder.java:41-44, JEC/ErasureDecoder.java:36-38
+    for (int j = 0; j < op.cols; ++j) {
+        if (op.lens && op.lens[j] > len) return ELECT_EC_EINVAL;
+        if (!op.in[j] && !(op.lens && op.lens[j] == 0)) return ELECT_EC_EINVAL;
+    }
+    for (int r = 0; r < op.rows; ++r)
+        if (!op.out[r]) return ELECT_EC_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return ELECT_EC_ENODEV;
+    int dev = 0;
+    int rc = host_device(ndev, &dev);
+    if (rc != ELECT_EC_OK) return rc;
+    if (dev < 0 || dev >= kMaxDevices || dev >= ndev) return ELECT_EC_ENODEV;
+    int prev = 0;
+    hipError_t e = hipGetDevice(&prev);
+    if (e == hipSuccess && prev != dev) e = hipSetDevice(dev);
+    if (e != hipSuccess) return map_hip(e);
+    rc = Batcher::kFallback;
+    if (batch_config().enabled.load() == 1 && !op.update && !op.lens && !op.hashes) {
+        Batcher* b = batcher(dev);
+        rc = b ? b->submit(op, len) : ELECT_EC_ENOMEM;
+    }
+    if (rc == Batcher::kFallback) {
+        if (!t_engines[dev]) t_engines[dev].reset(new (std::nothrow) HostEngine(dev));
+        rc = t_engines[dev] ? t_engines[dev]->run(op, len) : ELECT_EC_ENOMEM;
+    }
+    if (prev != dev) (void)hipSetDevice(prev);  // the caller's current device is left as it was
+    return rc;
+}
+
+int set_host_devices(const int* devices, int n)
+{
+    if (n < 0 || (n > 0 && !devices)) return ELECT_EC_EINVAL;
+    int ndev = 0;
+    if (n > 0 && (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)) return ELECT_EC_ENODEV;
+    for (int i = 0; i < n; ++i)
+        if (devices[i] < 0 || devices[i] >= ndev || devices[i] >= kMaxDevices) return ELECT_EC_EINVAL;
+    DevicePolicy& p = policy();
+    std::lock_guard<std::mutex> lock(p.mu);
+    p.env_read = true;  // an explicit list overrides the environment
+    p.devices.assign(devices, devices + n);
+    p.next = 0;
+    p.generation++;  // threads pick a device again on their next call
+    return ELECT_EC_OK;
+}
+
+int set_batching(int enable, unsigned window_us, size_t arena_bytes)
+{
+    if (enable < 0 || (enable && arena_bytes < (size_t{1} << 20))) return ELECT_EC_EINVAL;
+    BatchConfig& c = batch_config();
+    c.window_us = window_us;
+    if (arena_bytes) c.arena_bytes = arena_bytes;
+    c.enabled = enable ? 1 : 0;
+    return ELECT_EC_OK;
+}
+
+}  // namespace host
+}  // namespace elect

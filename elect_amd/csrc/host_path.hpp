@@ -1,0 +1,56 @@
+// host_path.hpp — the host-memory (JNI calling convention) path of the C ABI:
+// pinned staging, per-thread streams, device policy, cross-thread batching.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/elect_ec.h"
+#include "rs_kernels.hpp"
+
+namespace elect {
+namespace host {
+
+inline int map_hip(hipError_t e)
+{
+    switch (e) {
+    case hipSuccess: return ELECT_EC_OK;
+    case hipErrorNoDevice:
+    case hipErrorInvalidDevice:
+    case hipErrorNoBinaryForGpu: return ELECT_EC_ENODEV;
+    case hipErrorOutOfMemory: return ELECT_EC_ENOMEM;
+    case hipErrorInvalidValue: return ELECT_EC_EINVAL;
+    default: return ELECT_EC_EDEVICE;
+    }
+}
+
+inline kern::Column col(const void* base, size_t stripe_stride, size_t offset)
+{
+    kern::Column c;
+    c.ptr = static_cast<const uint8_t*>(base) + offset;
+    c.stride = stripe_stride;
+    return c;
+}
+
+// One synchronous host-memory operation: `cols` host inputs -> `rows` host outputs.
+struct HostOp {
+    int cols = 0;
+    int rows = 0;
+    bool update = false;  // cols = 2 + rows: [old, new, P...]; else an apply
+    const unsigned char* const* in = nullptr;
+    unsigned char* const* out = nullptr;
+    uint8_t coef[kern::kMaxRows * kern::kMaxCols] = {};
+    const size_t* lens = nullptr;  // optional content length per input (implicit zero padding)
+    int32_t* hashes = nullptr;     // optional host output: ByteBuffer.hashCode() per output row
+};
+
+// Runs op on the calling thread's device (or its assigned one, see
+// set_host_devices), through cross-thread batching when that is enabled.
+int run_host(const HostOp& op, size_t len);
+int set_host_devices(const int* devices, int n);
+int set_batching(int enable, unsigned window_us, size_t arena_bytes);
+
+}  // namespace host
+}  // namespace elect

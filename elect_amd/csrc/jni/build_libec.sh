@@ -15,7 +15,9 @@ gcc -O2 -fPIC -Wall -c -I"$JAVA_HOME/include" -I"$JAVA_HOME/include/linux" -I"$R
 "$HIPCC" --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/include" -x hip -c \
     "$ROOT/elect_amd/csrc/ec_capi.cpp" -o "$OUT/ec_capi.o"
 "$HIPCC" --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/include" -x hip -c \
+    "$ROOT/elect_amd/csrc/host_path.cpp" -o "$OUT/host_path.o"
+"$HIPCC" --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/include" -x hip -c \
     "$ROOT/elect_amd/csrc/rs_kernels.hip" -o "$OUT/rs_kernels.o"
 "$HIPCC" --offload-arch=gfx950 -shared -fPIC -o "$OUT/libec.so" \
-    "$OUT/libec_jni.o" "$OUT/ec_capi.o" "$OUT/rs_kernels.o"
+    "$OUT/libec_jni.o" "$OUT/ec_capi.o" "$OUT/host_path.o" "$OUT/rs_kernels.o"
 echo "built $OUT/libec.so — copy it to \$CASSANDRA_HOME/lib/sigar-bin (README.md:60)"

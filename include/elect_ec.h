@@ -84,6 +84,15 @@ int elect_ec_device_count(int* count);
  * n = 0 restores the default.  Returns ELECT_EC_EINVAL for an unknown device. */
 int elect_ec_set_host_devices(const int* devices, int n);
 
+/* Cross-thread batching of host-memory calls (off by default; or
+ * ELECT_EC_BATCH=1, ELECT_EC_BATCH_WINDOW_US, ELECT_EC_BATCH_ARENA_MB).  While
+ * on, concurrent elect_ec_encode / elect_ec_decode calls of the same shape made
+ * within window_us of each other share one pinned arena (arena_bytes of input
+ * per device, x2 for double buffering), one H2D, one kernel launch and one
+ * D2H; each call still returns only when its own outputs are written.  ELECT
+ * issues up to concurrent_ec (64) such calls at once (conf/elect.yaml:598). */
+int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes);
+
 /* ---- coder lifecycle ----
  * Replaces initEncoder / initDecoder (EC/erasure_coder.c:49-72) as called by
  * NativeRSEncoder_initImpl (EC/NativeRSEncoder.c:31-40) and NativeRSDecoder_initImpl

@@ -485,3 +485,53 @@ def test_mixed_size_batch_properties(dev, oracle):
             h = st[s].cpu().numpy()
             want = enc.encode([h[j] for j in range(k)])
             assert np.array_equal(h[k], want[0]) and np.array_equal(h[k + 1], want[1])
+
+
+def test_cross_thread_batching(dev, oracle):
+    """elect_ec_set_batching: concurrent one-stripe host calls share one arena,
+    H2D, launch and D2H.  Mixed shapes (two lengths, encode and decode) force
+    batches to close early and the two arenas to alternate; every call must
+    still get exactly its own parity / rebuilt unit."""
+    import threading
+    from elect_amd import _lib
+    from elect_amd.coder import RSCoder
+    k, m = 4, 2
+    coder = RSCoder(k, m)
+    enc = oracle.Encoder(k, m)
+    errors = []
+    _lib.set_batching(True, window_us=300, arena_bytes=8 << 20)
+    try:
+        def worker(t):
+            try:
+                L = 65536 + 48 if t % 3 else 4099
+                rng = np.random.default_rng(1000 + t)
+                for it in range(4):
+                    d = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+                    p = [np.empty(L, np.uint8) for _ in range(m)]
+                    coder.encode_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L)
+                    want = enc.encode(d)
+                    if not all(np.array_equal(a, b) for a, b in zip(p, want)):
+                        errors.append(f"t{t} it{it} parity")
+                    out = np.empty(L, np.uint8)
+                    coder.decode_host([p[0].ctypes.data] + [x.ctypes.data for x in d[1:]], [4, 1, 2, 3], [0],
+                                      [out.ctypes.data], L)
+                    if not np.array_equal(out, d[0]):
+                        errors.append(f"t{t} it{it} decode")
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(24)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        # a stripe larger than the arena falls back to the direct path
+        L = 3 << 20
+        d = [np.full(L, j + 1, np.uint8) for j in range(k)]
+        p = [np.empty(L, np.uint8) for _ in range(m)]
+        coder.encode_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L)
+        want = enc.encode(d)
+        assert all(np.array_equal(a, b) for a, b in zip(p, want))
+    finally:
+        _lib.set_batching(False)
+    assert not errors, errors[:5]

@@ -36,6 +36,10 @@ for step in "$@"; do
             -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $? ;;
     tune) run tune 600 tools/tune/tune_apply || exit $? ;;
     hostsweep) run hostsweep 600 python tools/tune/host_sweep.py || exit $? ;;
+    batching)
+        for L in 4404020 65536; do for T in 16 64; do for B in "" "--batch"; do
+            run "bench_hostpath_L${L}_T${T}${B}" 300 python bench.py --config hostpath --threads $T --host-chunk $L $B || exit $?
+        done; done; done ;;
     configs)
         run bench_mixed 400 python bench.py --config mixed || exit $?
         run bench_rs12 400 python bench.py --config rs12 || exit $?
