@@ -139,7 +139,7 @@ def set_host_devices(devices) -> None:
           "set_host_devices")
 
 
-def set_batching(enable: bool, window_us: int = 500, arena_bytes: int = 256 << 20) -> None:
+def set_batching(enable: bool, window_us: int = 0, arena_bytes: int = 256 << 20) -> None:
     """Cross-thread batching of concurrent host-memory encodes/decodes of one shape."""
     check(lib.elect_ec_set_batching(int(enable), window_us, arena_bytes), "set_batching")
 

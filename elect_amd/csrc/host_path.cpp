@@ -276,7 +276,7 @@ int host_device(int ndev, int* dev)
 // ---------------------------------------------------------------------------
 struct BatchConfig {
     std::atomic<int> enabled{-1};  // -1: read ELECT_EC_BATCH on first use
-    std::atomic<unsigned> window_us{500};
+    std::atomic<unsigned> window_us{0};
     std::atomic<size_t> arena_bytes{size_t{256} << 20};
 };
 
@@ -298,36 +298,32 @@ BatchConfig& batch_config()
 class Batcher {
 public:
     static constexpr int kFallback = 1000;  // request does not fit: run it directly
+    static constexpr int kSlabs = 2;
 
     explicit Batcher(int dev) : dev_(dev) {}
 
     int submit(const HostOp& op, size_t len)
     {
-        const BatchConfig& cfg = batch_config();
         const size_t pitch = (len + 255) & ~size_t{255};
-        const size_t arena = cfg.arena_bytes.load();
-        if (static_cast<size_t>(op.cols) * pitch > arena) return kFallback;
-
         std::unique_lock<std::mutex> lock(mu_);
-        if (!started_) {
+        if (!started_) {  // arenas, streams and events once, before anything is in flight
+            const int rc = init(batch_config().arena_bytes.load());
+            if (rc != ELECT_EC_OK) return rc;
             std::thread(&Batcher::worker, this).detach();  // lives as long as the process
             started_ = true;
         }
+        if (static_cast<size_t>(op.cols) * pitch > arena_ || static_cast<size_t>(op.rows) * pitch > arena_)
+            return kFallback;
         Slab* slab = nullptr;
-        int slot = -1;
         for (;;) {
             for (Slab& s : slabs_)
-                if (s.state == Slab::kOpen && s.matches(op, len) && s.reserved < s.capacity) {
-                    slab = &s;
-                    break;
-                }
+                if (s.state == Slab::kOpen && s.matches(op, len) && s.reserved < s.capacity) slab = &s;
             if (!slab) {
                 for (Slab& s : slabs_)  // a different shape or a full arena closes the open batch
-                    if (s.state == Slab::kOpen) s.state = Slab::kClosed;
+                    if (s.state == Slab::kOpen) s.full = true;
                 for (Slab& s : slabs_)
                     if (s.state == Slab::kFree) {
-                        const int rc = s.open(op, len, pitch, arena);
-                        if (rc != ELECT_EC_OK) return rc;
+                        s.open(op, len, pitch, arena_, ++opened_);
                         slab = &s;
                         break;
                     }
@@ -336,8 +332,9 @@ public:
             cv_.notify_all();
             cv_.wait(lock);
         }
-        slot = slab->reserved++;
+        const int slot = slab->reserved++;
         slab->readers++;
+        if (slab->reserved == slab->capacity) slab->full = true;
         cv_.notify_all();
         lock.unlock();
 
@@ -366,95 +363,103 @@ public:
 
 private:
     struct Slab {
-        enum State { kFree, kOpen, kClosed, kInFlight, kDone } state = kFree;
+        enum State { kFree, kOpen, kInFlight, kDone } state = kFree;
+        Batcher* owner = nullptr;
         int cols = 0, rows = 0;
         size_t len = 0, pitch = 0;
         uint8_t coef[kern::kMaxRows * kern::kMaxCols] = {};
         int capacity = 0, reserved = 0, filled = 0, readers = 0, status = ELECT_EC_OK;
+        bool full = false;
+        uint64_t seq = 0;
         std::chrono::steady_clock::time_point opened;
         uint8_t *pin_in = nullptr, *pin_out = nullptr, *d_in = nullptr, *d_out = nullptr;
-        size_t cap_in = 0, cap_out = 0;
         hipStream_t stream = nullptr;
+        hipEvent_t h2d_done = nullptr;
 
         bool matches(const HostOp& op, size_t n) const
         {
-            return op.cols == cols && op.rows == rows && n == len &&
-                   std::memcmp(op.coef, coef, sizeof(coef)) == 0;
+            return op.cols == cols && op.rows == rows && n == len && std::memcmp(op.coef, coef, sizeof(coef)) == 0;
         }
 
-        int open(const HostOp& op, size_t n, size_t p, size_t arena)
+        void open(const HostOp& op, size_t n, size_t p, size_t arena, uint64_t order)
         {
             cols = op.cols;
             rows = op.rows;
             len = n;
             pitch = p;
             std::memcpy(coef, op.coef, sizeof(coef));
-            capacity = static_cast<int>(arena / (static_cast<size_t>(cols) * pitch));
-            const size_t need_in = static_cast<size_t>(capacity) * cols * pitch;
-            const size_t need_out = static_cast<size_t>(capacity) * rows * pitch;
-            hipError_t e = hipSuccess;
-            if (!stream) e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
-            if (e == hipSuccess && need_in > cap_in) {
-                if (pin_in) (void)hipHostFree(pin_in);
-                if (d_in) (void)hipFree(d_in);
-                pin_in = d_in = nullptr;
-                cap_in = 0;
-                e = hipHostMalloc(reinterpret_cast<void**>(&pin_in), need_in, hipHostMallocDefault);
-                if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_in), need_in);
-                if (e == hipSuccess) cap_in = need_in;
-            }
-            if (e == hipSuccess && need_out > cap_out) {
-                if (pin_out) (void)hipHostFree(pin_out);
-                if (d_out) (void)hipFree(d_out);
-                pin_out = d_out = nullptr;
-                cap_out = 0;
-                e = hipHostMalloc(reinterpret_cast<void**>(&pin_out), need_out, hipHostMallocDefault);
-                if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_out), need_out);
-                if (e == hipSuccess) cap_out = need_out;
-            }
-            if (e != hipSuccess) return map_hip(e);
+            capacity = static_cast<int>(arena / (static_cast<size_t>(std::max(cols, rows)) * pitch));
             reserved = filled = readers = 0;
             status = ELECT_EC_OK;
+            full = false;
+            seq = order;
             opened = std::chrono::steady_clock::now();
             state = kOpen;
-            return ELECT_EC_OK;
         }
     };
 
+    int init(size_t arena)
+    {
+        arena_ = arena;
+        for (Slab& s : slabs_) {
+            s.owner = this;
+            hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_in), arena, hipHostMallocDefault);
+            if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_out), arena, hipHostMallocDefault);
+            if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_in), arena);
+            if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_out), arena);
+            if (e != hipSuccess) return map_hip(e);
+        }
+        return ELECT_EC_OK;
+    }
+
+    // Self-clocking dispatch: a batch leaves as soon as the previous batch's
+    // inputs have landed on the device (or at once on an idle device), so the
+    // next H2D overlaps the previous kernel and D2H; callers keep filling the
+    // other arena meanwhile.  An optional window (ELECT_EC_BATCH_WINDOW_US) caps
+    // how long an idle device waits for more callers; 0 = never wait.
     void worker()
     {
         (void)hipSetDevice(dev_);
+        Slab* prev = nullptr;
         std::unique_lock<std::mutex> lock(mu_);
         for (;;) {
             Slab* s = nullptr;
             cv_.wait(lock, [&] {
                 s = nullptr;
                 for (Slab& x : slabs_)
-                    if ((x.state == Slab::kOpen || x.state == Slab::kClosed) && (!s || x.opened < s->opened)) s = &x;
+                    if (x.state == Slab::kOpen && (!s || x.seq < s->seq)) s = &x;
                 return s != nullptr;
             });
-            // collect for the window (or until the arena is full), then wait for every copy-in
-            const auto deadline = s->opened + std::chrono::microseconds(batch_config().window_us.load());
-            cv_.wait_until(lock, deadline, [&] { return s->state != Slab::kOpen || s->reserved >= s->capacity; });
-            s->state = Slab::kClosed;
+            if (prev && prev->state == Slab::kInFlight) {  // wait for its H2D only
+                hipEvent_t ev = prev->h2d_done;
+                lock.unlock();
+                (void)hipEventSynchronize(ev);
+                lock.lock();
+            } else {
+                const unsigned w = batch_config().window_us.load();
+                if (w) cv_.wait_until(lock, s->opened + std::chrono::microseconds(w), [&] { return s->full; });
+            }
+            s->full = true;
+            s->state = Slab::kInFlight;  // no more reservations
             cv_.wait(lock, [&] { return s->filled == s->reserved; });
-            s->state = Slab::kInFlight;
             const int n = s->reserved;
             lock.unlock();
-            const int rc = n > 0 ? code(*s, n) : ELECT_EC_OK;
+            const hipError_t e = issue(*s, n);
+            if (e != hipSuccess) (void)hipStreamSynchronize(s->stream);  // no callback was queued
             lock.lock();
-            s->status = rc;
-            s->state = Slab::kDone;
-            if (s->readers == 0) s->state = Slab::kFree;
-            cv_.notify_all();
+            if (e != hipSuccess) finish(s, map_hip(e));
+            prev = s;
         }
     }
 
-    static int code(Slab& s, int n)
+    static hipError_t issue(Slab& s, int n)
     {
         const size_t in_stride = static_cast<size_t>(s.cols) * s.pitch;
         const size_t out_stride = static_cast<size_t>(s.rows) * s.pitch;
         hipError_t e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
+        if (e == hipSuccess) e = hipEventRecord(s.h2d_done, s.stream);
         if (e == hipSuccess) {
             ApplyParams p;
             p.len = s.len;
@@ -467,15 +472,31 @@ private:
             e = kern::launch_apply(p, s.stream);
         }
         if (e == hipSuccess) e = hipMemcpyAsync(s.pin_out, s.d_out, n * out_stride, hipMemcpyDeviceToHost, s.stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
-        return map_hip(e);
+        if (e == hipSuccess) e = hipLaunchHostFunc(s.stream, &Batcher::on_done, &s);
+        return e;
+    }
+
+    static void on_done(void* arg)  // HIP host-function callback: no HIP calls in here
+    {
+        Slab* s = static_cast<Slab*>(arg);
+        std::lock_guard<std::mutex> lock(s->owner->mu_);
+        s->owner->finish(s, ELECT_EC_OK);
+    }
+
+    void finish(Slab* s, int status)  // mu_ held
+    {
+        s->status = status;
+        s->state = s->readers == 0 ? Slab::kFree : Slab::kDone;
+        cv_.notify_all();
     }
 
     int dev_;
     std::mutex mu_;
     std::condition_variable cv_;
     bool started_ = false;
-    Slab slabs_[2];
+    size_t arena_ = 0;
+    uint64_t opened_ = 0;
+    Slab slabs_[kSlabs];
 };
 
 Batcher* batcher(int dev)

@@ -86,11 +86,14 @@ int elect_ec_set_host_devices(const int* devices, int n);
 
 /* Cross-thread batching of host-memory calls (off by default; or
  * ELECT_EC_BATCH=1, ELECT_EC_BATCH_WINDOW_US, ELECT_EC_BATCH_ARENA_MB).  While
- * on, concurrent elect_ec_encode / elect_ec_decode calls of the same shape made
- * within window_us of each other share one pinned arena (arena_bytes of input
- * per device, x2 for double buffering), one H2D, one kernel launch and one
- * D2H; each call still returns only when its own outputs are written.  ELECT
- * issues up to concurrent_ec (64) such calls at once (conf/elect.yaml:598). */
+ * on, concurrent elect_ec_encode / elect_ec_decode calls of the same shape share
+ * one pinned arena, one H2D, one kernel launch and one D2H; each call still
+ * returns only when its own outputs are written.  Dispatch is self-clocking: a
+ * batch leaves when the previous batch's inputs are on the device (at once on
+ * an idle device, or after window_us if non-zero), so transfers pipeline.
+ * arena_bytes (per direction, x2 arenas, per device) takes effect for devices
+ * whose batcher has not started yet.  ELECT issues up to concurrent_ec (64)
+ * such calls at once (conf/elect.yaml:598). */
 int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes);
 
 /* ---- coder lifecycle ----
