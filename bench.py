@@ -386,7 +386,8 @@ def config_hashed(args, world, rank, dev):
     (java.nio.ByteBuffer.hashCode of every parity unit), 64 KiB, 4096 stripes."""
     from elect_amd.batch import encode_batch, encode_batch_hashed
     from elect_amd.coder import RSCoder
-    k, m, L, B = 4, 2, 65536, 4096
+    k, m, L = 4, 2, args.chunk
+    B = max(1, (1 << 30) // (k * L))  # 1 GiB of data per GPU
     coder = RSCoder(k, m)
     data = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev)
     par = torch.empty((B, m, L), dtype=torch.uint8, device=dev)
@@ -411,7 +412,7 @@ def config_hashed(args, world, rank, dev):
                                        for s, r in ((0, 0), (B - 1, m - 1)))
     alg = B * (k + m) * L
     gbs = alg / (ms * 1e-3) / 1e9
-    return {"metric": "GiB/s device-resident RS(6,4) encode + fused parity hashCode, 64 KiB chunks",
+    return {"metric": f"GiB/s device-resident RS(6,4) encode + fused parity hashCode, {L} B chunks",
             "value": round(world * args.steps * B * k * L / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",

@@ -213,6 +213,7 @@ struct FastArgs {
     int32_t* hashes;        // optional parity hashes, [stripe][hstride] (row r at +r)
     uint32_t hstride;
     uint64_t hbase;
+    uint32_t* hpart;        // per-wave partial sums [wave][R] (waves wholly inside one stripe)
     gf::PermTable tab[R][K];
 };
 
@@ -319,15 +320,14 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         const uint32_t s_first = static_cast<uint32_t>((static_cast<uint64_t>(first) * a.magic) >> a.shift);
         const uint32_t s_last = static_cast<uint32_t>((static_cast<uint64_t>(last) * a.magic) >> a.shift);
         const bool whole_wave = last < a.total && s_first == s_last;  // wave-uniform
-        if (whole_wave) {
+        if (whole_wave) {  // partial sums to scratch; hash_reduce adds them per stripe
             const uint32_t seg0 = first - s_first * a.segs;
             const uint32_t p0 = dpow31(a.hbase + static_cast<uint64_t>(seg0) * 16);
             const uint32_t q = kLanePow.v[threadIdx.x & 63u] * p0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const uint32_t sum = wave_sum(horner31(acc[r]) * q);
-                if ((threadIdx.x & 63u) == 0)
-                    atomicAdd(reinterpret_cast<unsigned*>(a.hashes) + static_cast<uint64_t>(stripe) * a.hstride + r, sum);
+                if ((threadIdx.x & 63u) == 0) a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum;
             }
         } else {
             const uint32_t p = dpow31(a.hbase + off);
@@ -337,6 +337,23 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
                           horner31(acc[r]) * p);
         }
     }
+}
+
+// Sum the per-wave hash partials of each (stripe, row): the waves lying wholly
+// inside stripe s are [ceil(s*segs/64), floor((s+1)*segs/64)); straddling waves
+// already added theirs atomically.  One thread per (stripe, row), sole writer.
+__global__ __launch_bounds__(kBlock) void hash_reduce(const uint32_t* __restrict__ part, int32_t* hashes,
+                                                      uint32_t hstride, int rows, uint32_t segs, uint32_t stripes)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= stripes * static_cast<uint32_t>(rows)) return;
+    const uint32_t s = t / rows, r = t % rows;
+    const uint64_t w0 = (static_cast<uint64_t>(s) * segs + 63) / 64;
+    const uint64_t w1 = (static_cast<uint64_t>(s) + 1) * segs / 64;
+    uint32_t sum = 0;
+    for (uint64_t w = w0; w < w1; ++w) sum += part[w * rows + r];
+    uint32_t* h = reinterpret_cast<uint32_t*>(hashes) + static_cast<uint64_t>(s) * hstride + r;
+    *h += sum;
 }
 
 // Small chunks (<= 4 KiB per shard) ran 3-4 % faster with 128-thread blocks.
@@ -376,9 +393,25 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         a.lens = p.lens ? p.lens + s0 * p.cols : nullptr;
         a.hashes = p.hashes ? p.hashes + s0 * p.hash_stride + r0 : nullptr;
         a.total = static_cast<uint32_t>(ns * segs64);
+        a.hpart = nullptr;
+        if (a.hashes) {  // stream-ordered scratch for the per-wave partial sums
+            const size_t bytes = (static_cast<size_t>(a.total) / 64 + 1) * R * sizeof(uint32_t);
+            const hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&a.hpart), bytes, stream);
+            if (e != hipSuccess) return e;
+        }
         const uint32_t grid = (a.total + block - 1) / block;
         hipLaunchKernelGGL((gf_apply_x16<K, R, PAD>), dim3(grid), dim3(block), 0, stream, a);
-        const hipError_t e = hipGetLastError();
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess && a.hashes) {
+            const uint32_t n = static_cast<uint32_t>(ns) * R;
+            hipLaunchKernelGGL(hash_reduce, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, a.hpart,
+                               a.hashes, a.hstride, R, a.segs, static_cast<uint32_t>(ns));
+            e = hipGetLastError();
+        }
+        if (a.hpart) {
+            const hipError_t f = hipFreeAsync(a.hpart, stream);
+            if (e == hipSuccess) e = f;
+        }
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

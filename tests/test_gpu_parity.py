@@ -356,7 +356,7 @@ def test_host_path_concurrent_callers(dev, oracle):
     assert not errors, errors
 
 
-@pytest.mark.parametrize("k,m,L", [(4, 2, 65536), (4, 2, 4099), (4, 2, 1), (4, 2, 15), (8, 4, 1024),
+@pytest.mark.parametrize("k,m,L", [(4, 2, 65536), (4, 2, 4099), (4, 2, 1), (4, 2, 15), (8, 4, 1024), (4, 2, 1 << 20),
                                    (4, 10, 333), (3, 2, 4404020 // 64)])
 def test_encode_batch_hashed_matches_java_hashcode(dev, oracle, k, m, L):
     """Fused parity hash == java.nio.ByteBuffer.hashCode() of each parity unit

@@ -35,6 +35,7 @@ for step in "$@"; do
         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run \
             -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $? ;;
     tune) run tune 600 tools/tune/tune_apply || exit $? ;;
+    probe) run probe 300 tools/tune/tune_apply probe || exit $? ;;
     hostsweep) run hostsweep 600 python tools/tune/host_sweep.py || exit $? ;;
     batching)
         for L in 4404020 65536; do for T in 16 64; do for B in "" "--batch"; do
@@ -46,7 +47,8 @@ for step in "$@"; do
         run bench_hostpath 400 python bench.py --config hostpath || exit $?
         run bench_update 400 python bench.py --config update || exit $?
         run bench_padded 400 python bench.py --config padded || exit $?
-        run bench_hashed 400 python bench.py --config hashed || exit $? ;;
+        run bench_hashed 400 python bench.py --config hashed || exit $?
+        run bench_hashed_1M 400 python bench.py --config hashed --chunk 1048576 || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

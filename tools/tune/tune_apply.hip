@@ -66,7 +66,35 @@ __device__ __forceinline__ void set_word(uint4& v, int w, uint32_t x)
     else v.w = x;
 }
 
-enum Mode { kGF = 0, kXor = 1 };
+enum Mode { kGF = 0, kXor = 1, kHashAtomic = 2, kHashScratch = 3, kHashLocal = 4 };
+
+__device__ __forceinline__ uint32_t dpow31(uint64_t e)
+{
+    uint32_t r = 1, b = 31;
+    for (; e; e >>= 1, b *= b)
+        if (e & 1) r *= b;
+    return r;
+}
+__device__ __forceinline__ uint32_t horner31(const uint4& v)
+{
+    uint32_t h = 0;
+#pragma unroll
+    for (int w = 3; w >= 0; --w) {
+        const int x = static_cast<int>(lane_word(v, w));
+        const int lo = __builtin_amdgcn_sdot4(x, 0x00001F01, 0, false);
+        const int hi = __builtin_amdgcn_sdot4(x, 0x1F010000, 0, false);
+        const uint32_t d = static_cast<uint32_t>(__mul24(hi, 961) + lo);
+        h = w == 3 ? d : h * 923521u + d;
+    }
+    return h;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d, 64));
+    return v;
+}
+__device__ uint32_t* g_hash;  // set by the host before hash variants run
 enum Load { kPlain = 0, kNTL = 1, kNTS = 2, kNT = 3 };
 
 template <int K, int R, int U, int BLOCK, int MODE, int LD, bool GRIDSTRIDE, int ORDER = 0>
@@ -109,7 +137,7 @@ __global__ __launch_bounds__(BLOCK) void kern(const Args<K, R> a)
         for (int u = 0; u < U; ++u) {
             if (!live[u]) continue;
             uint4 acc[R];
-            if (ORDER == 2 && MODE == kGF) {
+            if (ORDER == 2 && (MODE == kGF || MODE >= kHashAtomic)) {
 #pragma unroll
                 for (int j = 0; j < K; ++j) {
                     uint32_t s0[4], s1[4], s2[4];
@@ -189,6 +217,26 @@ __global__ __launch_bounds__(BLOCK) void kern(const Args<K, R> a)
                 if (LD & kNTS) nt_store(acc[r], p);
                 else *p = acc[r];
             }
+            if (MODE >= kHashAtomic) {
+                const uint32_t idx = first + u * BLOCK;
+                const uint32_t f = __builtin_amdgcn_readfirstlane(idx);
+                const uint32_t s0 = static_cast<uint32_t>((static_cast<uint64_t>(f) * a.magic) >> a.shift);
+                const uint32_t seg0 = f - s0 * a.segs;
+                const uint32_t q = dpow31(16u * (threadIdx.x & 63u)) * dpow31(static_cast<uint64_t>(seg0) * 16);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t hv = horner31(acc[r]) * q;
+                    if (MODE == kHashLocal) {
+                        if (hv == 0x12345678u) g_hash[0] = hv;  // compute only
+                    } else {
+                        const uint32_t sum = wave_sum(hv);
+                        if ((threadIdx.x & 63u) == 0) {
+                            if (MODE == kHashAtomic) atomicAdd(g_hash + static_cast<uint64_t>(stripe[u]) * R + r, sum);
+                            else g_hash[(static_cast<uint64_t>(idx) >> 6) * R + r] = sum;
+                        }
+                    }
+                }
+            }
         }
         if (!GRIDSTRIDE) break;
     }
@@ -257,6 +305,9 @@ struct Runner {
         hipDeviceProp_t prop;
         CK(hipGetDeviceProperties(&prop, 0));
         dev_cus = prop.multiProcessorCount;
+        uint32_t* hbuf = nullptr;
+        CK(hipMalloc(&hbuf, (static_cast<uint64_t>(a.total) / 64 + 64) * 4 * 4 + s.B * 16));
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_hash), &hbuf, sizeof(hbuf)));
     }
 
     template <int U, int BLOCK, int MODE, int LD, bool GS, int ORDER = 0>
@@ -344,6 +395,9 @@ static void sweep(const Shape& s)
         rec("U1 b128 ntboth LDS-tab", rn.template time_one<1, 128, kGF, kNT, false, 2>(0, it), true);
         rec("U1 b128 ntboth colorder", rn.template time_one<1, 128, kGF, kNT, false, 1>(0, it), true);
         rec("U1 b128 ntload colorder", rn.template time_one<1, 128, kGF, kNTL, false, 1>(0, it), true);
+        rec("U1 nt LDS hash-atomic", rn.template time_one<1, 256, kHashAtomic, kNT, false, 2>(0, it), true);
+        rec("U1 nt LDS hash-scratch", rn.template time_one<1, 256, kHashScratch, kNT, false, 2>(0, it), true);
+        rec("U1 nt LDS hash-compute", rn.template time_one<1, 256, kHashLocal, kNT, false, 2>(0, it), true);
         rec("U1 XOR-only ntload", rn.template time_one<1, 256, kXor, kNTL, false>(0, it), false);
         rec("U1 XOR-only nt both", rn.template time_one<1, 256, kXor, kNT, false>(0, it), false);
         // restore reference output for later variants' checks
@@ -364,8 +418,88 @@ __global__ void copy_kernel(const uint4* __restrict__ in, uint4* __restrict__ ou
     if (i < n) out[i] = in[i];
 }
 
-int main()
+template <bool NT>
+__global__ void read_kernel(const uint4* __restrict__ in, uint32_t* sink, uint64_t n)
 {
+    const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    const uint4 v = NT ? nt_load(in + i) : in[i];
+    if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9E3779B9u) sink[0] = 1;  // keeps the load live
+}
+
+template <bool NT>
+__global__ void write_kernel(uint4* __restrict__ out, uint64_t n)
+{
+    const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    const uint4 v = make_uint4(static_cast<uint32_t>(i), 1, 2, 3);
+    if (NT) nt_store(v, out + i);
+    else out[i] = v;
+}
+
+template <bool NT>
+__global__ void copy_kernel_nt(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n)
+{
+    const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    if (NT) nt_store(nt_load(in + i), out + i);
+    else out[i] = in[i];
+}
+
+template <class F>
+static float median_ms(F&& launch, int iters = 25)
+{
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> ts;
+    for (int i = 0; i < iters; ++i) {
+        CK(hipEventRecord(e0));
+        launch();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ts.push_back(ms);
+    }
+    std::sort(ts.begin(), ts.end());
+    return ts[ts.size() / 2];
+}
+
+static void hbm_probe()
+{
+    const uint64_t bytes = 2ull << 30, n = bytes / 16;
+    uint8_t *a, *b;
+    uint32_t* sink;
+    CK(hipMalloc(&a, bytes));
+    CK(hipMalloc(&b, bytes));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMemset(a, 7, bytes));
+    const dim3 g((n + 255) / 256);
+    auto rep = [&](const char* name, double moved, float ms) {
+        std::printf("probe %-22s %8.4f ms  %7.1f GB/s  %5.1f%% of 8 TB/s\n", name, ms, moved / (ms * 1e-3) / 1e9,
+                    100.0 * moved / (ms * 1e-3) / 8e12);
+    };
+    for (int round = 0; round < 2; ++round) {
+        rep("read plain 2 GiB", bytes, median_ms([&] { hipLaunchKernelGGL(read_kernel<false>, g, dim3(256), 0, 0, (const uint4*)a, sink, n); }));
+        rep("read nt 2 GiB", bytes, median_ms([&] { hipLaunchKernelGGL(read_kernel<true>, g, dim3(256), 0, 0, (const uint4*)a, sink, n); }));
+        rep("write plain 2 GiB", bytes, median_ms([&] { hipLaunchKernelGGL(write_kernel<false>, g, dim3(256), 0, 0, (uint4*)b, n); }));
+        rep("write nt 2 GiB", bytes, median_ms([&] { hipLaunchKernelGGL(write_kernel<true>, g, dim3(256), 0, 0, (uint4*)b, n); }));
+        rep("copy plain 2 GiB", 2.0 * bytes, median_ms([&] { hipLaunchKernelGGL(copy_kernel_nt<false>, g, dim3(256), 0, 0, (const uint4*)a, (uint4*)b, n); }));
+        rep("copy nt 2 GiB", 2.0 * bytes, median_ms([&] { hipLaunchKernelGGL(copy_kernel_nt<true>, g, dim3(256), 0, 0, (const uint4*)a, (uint4*)b, n); }));
+    }
+    CK(hipFree(a));
+    CK(hipFree(b));
+    CK(hipFree(sink));
+}
+
+int main(int argc, char** argv)
+{
+    if (argc > 1 && std::string(argv[1]) == "probe") {
+        hbm_probe();
+        return 0;
+    }
+    {
     int ndev = 0;
     CK(hipGetDeviceCount(&ndev));
     hipDeviceProp_t prop;
@@ -418,5 +552,6 @@ int main()
     sweep<4, 2>(Shape{"RS(6,4) encode 4KiB", 4, 2, 4096, 65536, 6});
     sweep<4, 2>(Shape{"RS(6,4) encode 1MiB", 4, 2, 1048576, 256, 6});
     sweep<4, 1>(Shape{"RS(6,4) decode e=1 1KiB", 4, 1, 1024, 262144, 6});
+    }
     return 0;
 }
