@@ -341,19 +341,23 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 
 // Sum the per-wave hash partials of each (stripe, row): the waves lying wholly
 // inside stripe s are [ceil(s*segs/64), floor((s+1)*segs/64)); straddling waves
-// already added theirs atomically.  One thread per (stripe, row), sole writer.
+// already added theirs atomically.  One wave per (stripe, row): lanes stride
+// over the partials, then a wave sum; lane 0 is the sole writer.
 __global__ __launch_bounds__(kBlock) void hash_reduce(const uint32_t* __restrict__ part, int32_t* hashes,
                                                       uint32_t hstride, int rows, uint32_t segs, uint32_t stripes)
 {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // (stripe, row) of this wave
     if (t >= stripes * static_cast<uint32_t>(rows)) return;
-    const uint32_t s = t / rows, r = t % rows;
+    const uint32_t s = t / rows, r = t % rows, lane = threadIdx.x & 63u;
     const uint64_t w0 = (static_cast<uint64_t>(s) * segs + 63) / 64;
     const uint64_t w1 = (static_cast<uint64_t>(s) + 1) * segs / 64;
     uint32_t sum = 0;
-    for (uint64_t w = w0; w < w1; ++w) sum += part[w * rows + r];
-    uint32_t* h = reinterpret_cast<uint32_t*>(hashes) + static_cast<uint64_t>(s) * hstride + r;
-    *h += sum;
+    for (uint64_t w = w0 + lane; w < w1; w += 64) sum += part[w * rows + r];
+    sum = wave_sum(sum);
+    if (lane == 0) {
+        uint32_t* h = reinterpret_cast<uint32_t*>(hashes) + static_cast<uint64_t>(s) * hstride + r;
+        *h += sum;
+    }
 }
 
 // Small chunks (<= 4 KiB per shard) ran 3-4 % faster with 128-thread blocks.
@@ -403,8 +407,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         hipLaunchKernelGGL((gf_apply_x16<K, R, PAD>), dim3(grid), dim3(block), 0, stream, a);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess && a.hashes) {
-            const uint32_t n = static_cast<uint32_t>(ns) * R;
-            hipLaunchKernelGGL(hash_reduce, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, a.hpart,
+            const uint32_t n = static_cast<uint32_t>(ns) * R;  // one wave each
+            hipLaunchKernelGGL(hash_reduce, dim3((n + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, stream, a.hpart,
                                a.hashes, a.hstride, R, a.segs, static_cast<uint32_t>(ns));
             e = hipGetLastError();
         }
