@@ -36,6 +36,16 @@ for step in "$@"; do
             -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $? ;;
     tune) run tune 600 tools/tune/tune_apply || exit $? ;;
     probe) run probe 300 tools/tune/tune_apply probe || exit $? ;;
+    multirank)  # rehearse the N>1 flow: 2 ranks sharing the one GPU, gloo handshake
+        export ELECT_BENCH_BACKEND=gloo
+        run bench_rehearse_2rank 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu || exit $?
+        run bench_rehearse_2rank_mixed 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --config mixed --steps 10 || exit $?
+        unset ELECT_BENCH_BACKEND ;;
+    hashed)
+        run bench_hashed 400 python bench.py --config hashed || exit $?
+        run bench_hashed_1M 400 python bench.py --config hashed --chunk 1048576 || exit $? ;;
     hostsweep) run hostsweep 600 python tools/tune/host_sweep.py || exit $? ;;
     batching)
         for L in 4404020 65536; do for T in 16 64; do for B in "" "--batch"; do
