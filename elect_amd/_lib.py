@@ -10,7 +10,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libelect_ec.so")
+LIB_PATH = os.environ.get("ELECT_EC_LIB") or os.path.join(HERE, "libelect_ec.so")  # override: A/B builds
 
 OK = 0
 WARN_SINGULAR = 1

@@ -59,6 +59,13 @@ for step in "$@"; do
         run bench_padded 400 python bench.py --config padded || exit $?
         run bench_hashed 400 python bench.py --config hashed || exit $?
         run bench_hashed_1M 400 python bench.py --config hashed --chunk 1048576 || exit $? ;;
+    ab)  # A/B: in-tree lib vs elect_amd/_ab/libelect_ec_b.so (built by hand with the variant), interleaved
+        for i in 1 2 3; do for v in a b; do
+            lib=""; [ $v = b ] && lib="$PWD/elect_amd/_ab/libelect_ec_b.so"
+            for c in headline rs12 padded; do
+                ELECT_EC_LIB=$lib run "ab_${v}_${c}_$i" 300 python bench.py --config $c --no-cpu --no-host --steps 50 || exit $?
+            done
+        done; done ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
