@@ -116,7 +116,14 @@ def cpu_baseline(args, k, m, L):
         reps += 1
     assert np.array_equal(out[:, 0], buf[:, 0]), "CPU baseline decode mismatch"
     data_bytes = 2 * reps * stripes * k * L
+    # single-core figure: the same loop on one thread, ~3 s
+    t1, reps1 = 0.0, 0
+    while t1 < args.cpu_seconds * 0.3 or reps1 < 1:
+        t1 += orc.batch_apply(enc_coef, buf, sstride, enc_src, buf, sstride, enc_dst, L, stripes, 1, level)
+        t1 += orc.batch_apply(dec_coef, buf, sstride, dec_src, out, L, [0], L, stripes, 1, level)
+        reps1 += 1
     return {
+        "single_core_GiB/s": round(2 * reps1 * stripes * k * L / t1 / GIB, 3),
         "value": round(data_bytes / total_t / GIB, 3),
         "unit": "GiB/s",
         "cores": threads,
@@ -155,6 +162,45 @@ def host_inclusive(coder, k, m, L, stripes_total, dev):
         run()
     dt = time.perf_counter() - t0
     return round(reps * nchunks * chunk * k * L / dt / GIB, 2)
+
+
+def decode_sweep(coder, stripe, k, m, L, B, stream, reps=5):
+    """Single-erasure decode for each data shard j (survivors: the other k of
+    shards 0..k), outside the timed region: per-kernel GB/s and HBM fraction."""
+    from elect_amd.batch import decode_batch
+    out = torch.empty((B, 1, L), dtype=torch.uint8, device=stripe.device)
+    res = {}
+    for j in range(k):
+        surv = [i for i in range(k + 1) if i != j]
+        decode_batch(coder, stripe, surv, [j], out, inputs_by_unit=True, stream=stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            decode_batch(coder, stripe, surv, [j], out, inputs_by_unit=True, stream=stream)
+        e1.record(stream)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        gbs = B * (k + 1) * L / (ms * 1e-3) / 1e9
+        res[f"erase{j}"] = {"ms": round(ms, 4), "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                            "verified": bool(torch.equal(out[:, 0], stripe[:, j]))}
+    return res
+
+
+def device_copy_rate(dev, nbytes=1 << 30, reps=5):
+    """A plain device copy (torch copy_ of 1 GiB) as a measured HBM reference
+    next to the 8 TB/s peak; read + write bytes counted."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
 
 
 def timed(step, steps, warmup, world):
@@ -528,6 +574,11 @@ def main():
         },
         "verified": ok,
     }
+    if rank == 0:
+        out["kernels"]["decode_sweep"] = sw = decode_sweep(coder, stripe, k, m, L, B, stream)
+        ok = ok and all(v["verified"] for v in sw.values())
+        out["verified"] = ok
+        out["roofline"]["device_copy_GB/s"] = device_copy_rate(dev)
     if rank == 0 and not args.no_host:
         out["host_inclusive_GiB/s"] = host_inclusive(coder, k, m, L, min(B, 2048), dev)
     if rank == 0 and world == 1 and not args.no_cpu:

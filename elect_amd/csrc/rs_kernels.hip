@@ -259,15 +259,21 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         for (int j = 0; j < K; ++j) sl[j] = __builtin_amdgcn_readfirstlane(l[j]);
     }
 
-    for (int i = threadIdx.x; i < R * K; i += blockDim.x) {
-        const gf::PermTable& t = a.tab[i / K][i % K];
-        tl[i * kTabStride + 0] = t.t0_lo;
-        tl[i * kTabStride + 1] = t.t0_hi;
-        tl[i * kTabStride + 2] = t.t1_lo;
-        tl[i * kTabStride + 3] = t.t1_hi;
-        tl[i * kTabStride + 4] = t.t2;
+#ifndef AB_SGPR_MAX
+#define AB_SGPR_MAX 0
+#endif
+    constexpr bool kSgpr = R * K <= AB_SGPR_MAX;
+    if (!kSgpr) {
+        for (int i = threadIdx.x; i < R * K; i += blockDim.x) {
+            const gf::PermTable& t = a.tab[i / K][i % K];
+            tl[i * kTabStride + 0] = t.t0_lo;
+            tl[i * kTabStride + 1] = t.t0_hi;
+            tl[i * kTabStride + 2] = t.t1_lo;
+            tl[i * kTabStride + 3] = t.t1_hi;
+            tl[i * kTabStride + 4] = t.t2;
+        }
+        __syncthreads();
     }
-    __syncthreads();
     if (!live) return;
     if (!PAD) {
 #pragma unroll
@@ -317,8 +323,16 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const uint4 tq = *reinterpret_cast<const uint4*>(&tl[(r * K + j) * kTabStride]);
-            const uint32_t t2 = tl[(r * K + j) * kTabStride + 4];
+            uint4 tq;
+            uint32_t t2;
+            if (kSgpr) {
+                const gf::PermTable& t = a.tab[r][j];
+                tq = make_uint4(t.t0_lo, t.t0_hi, t.t1_lo, t.t1_hi);
+                t2 = t.t2;
+            } else {
+                tq = *reinterpret_cast<const uint4*>(&tl[(r * K + j) * kTabStride]);
+                t2 = tl[(r * K + j) * kTabStride + 4];
+            }
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
                 const uint32_t v = xor3(__builtin_amdgcn_perm(tq.y, tq.x, s0[w]),
@@ -396,7 +410,11 @@ __global__ __launch_bounds__(kBlock) void hash_reduce(const uint32_t* __restrict
 
 // Small chunks (<= 4 KiB per shard) ran 3-4 % faster with 128-thread blocks,
 // and so did 4-row launches (RS(12,8) encode, +2-3.5 % in two sweeps).
+#ifdef AB_BLOCK128
+inline int block_for(uint64_t, int) { return 128; }
+#else
 inline int block_for(uint64_t len, int rows) { return (len <= 4096 || rows >= 4) ? 128 : kBlock; }
+#endif
 
 template <int K, int R, bool PAD>
 hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)

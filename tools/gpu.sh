@@ -4,7 +4,7 @@
 cd "$(dirname "$0")/.."
 T=$1; shift
 rm -f gpurun_out/*.log gpurun_out/status.txt
-/usr/local/graft/bin/gpurun --timeout "$T" -- "tools/gpu_run.sh $*" > /tmp/gpurun_last.log 2>&1
+/usr/local/graft/bin/gpurun --timeout "$T" -- "${GPU_ENV:-} tools/gpu_run.sh $*" > /tmp/gpurun_last.log 2>&1
 rc=$?
 echo "gpurun exit=$rc"; sed -n 2,3p /tmp/gpurun_last.log
 [ -f gpurun_out/pytest_gpu.log ] && tail -2 gpurun_out/pytest_gpu.log

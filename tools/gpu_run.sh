@@ -35,7 +35,13 @@ for step in "$@"; do
         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run \
             -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $? ;;
     tune) run tune 600 tools/tune/tune_apply || exit $? ;;
+    envprobe)  # host facts for DESIGN.md: CPU model, ISA-L presence (for a dlopen cross-check)
+        { lscpu | grep -E "Model name|^CPU\(s\)|Flags" | cut -c1-200; echo "nproc=$(nproc)";
+          echo "isal: $(ldconfig -p 2>/dev/null | grep -ci isal) ldconfig entries";
+          ls /usr/lib/x86_64-linux-gnu /usr/local/lib /opt/rocm/lib 2>/dev/null | grep -i isal || echo "no libisal files"; } \
+            > gpurun_out/envprobe.log 2>&1; cat gpurun_out/envprobe.log ;;
     probe) run probe 300 tools/tune/tune_apply probe || exit $? ;;
+    streams) run streams 300 tools/tune/tune_apply streams || exit $? ;;
     multirank)  # rehearse the N>1 flow: 2 ranks sharing the one GPU, gloo handshake
         export ELECT_BENCH_BACKEND=gloo
         run bench_rehearse_2rank 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
@@ -59,10 +65,10 @@ for step in "$@"; do
         run bench_padded 400 python bench.py --config padded || exit $?
         run bench_hashed 400 python bench.py --config hashed || exit $?
         run bench_hashed_1M 400 python bench.py --config hashed --chunk 1048576 || exit $? ;;
-    ab)  # A/B: in-tree lib vs elect_amd/_ab/libelect_ec_b.so (built by hand with the variant), interleaved
-        for i in 1 2 3; do for v in a b; do
-            lib=""; [ $v = b ] && lib="$PWD/elect_amd/_ab/libelect_ec_b.so"
-            for c in headline rs12 padded; do
+    ab)  # A/B: in-tree lib ("a") vs elect_amd/_ab/libelect_ec_<v>.so for v in $AB_VARIANTS, interleaved
+        for i in 1 2 3; do for v in a ${AB_VARIANTS:-b}; do
+            lib=""; [ $v = a ] || lib="$PWD/elect_amd/_ab/libelect_ec_$v.so"
+            for c in ${AB_CONFIGS:-headline rs12 padded}; do
                 ELECT_EC_LIB=$lib run "ab_${v}_${c}_$i" 300 python bench.py --config $c --no-cpu --no-host --steps 50 || exit $?
             done
         done; done ;;
