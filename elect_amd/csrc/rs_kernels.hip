@@ -259,21 +259,15 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         for (int j = 0; j < K; ++j) sl[j] = __builtin_amdgcn_readfirstlane(l[j]);
     }
 
-#ifndef AB_SGPR_MAX
-#define AB_SGPR_MAX 0
-#endif
-    constexpr bool kSgpr = R * K <= AB_SGPR_MAX;
-    if (!kSgpr) {
-        for (int i = threadIdx.x; i < R * K; i += blockDim.x) {
-            const gf::PermTable& t = a.tab[i / K][i % K];
-            tl[i * kTabStride + 0] = t.t0_lo;
-            tl[i * kTabStride + 1] = t.t0_hi;
-            tl[i * kTabStride + 2] = t.t1_lo;
-            tl[i * kTabStride + 3] = t.t1_hi;
-            tl[i * kTabStride + 4] = t.t2;
-        }
-        __syncthreads();
+    for (int i = threadIdx.x; i < R * K; i += blockDim.x) {
+        const gf::PermTable& t = a.tab[i / K][i % K];
+        tl[i * kTabStride + 0] = t.t0_lo;
+        tl[i * kTabStride + 1] = t.t0_hi;
+        tl[i * kTabStride + 2] = t.t1_lo;
+        tl[i * kTabStride + 3] = t.t1_hi;
+        tl[i * kTabStride + 4] = t.t2;
     }
+    __syncthreads();
     if (!live) return;
     if (!PAD) {
 #pragma unroll
@@ -323,16 +317,8 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            uint4 tq;
-            uint32_t t2;
-            if (kSgpr) {
-                const gf::PermTable& t = a.tab[r][j];
-                tq = make_uint4(t.t0_lo, t.t0_hi, t.t1_lo, t.t1_hi);
-                t2 = t.t2;
-            } else {
-                tq = *reinterpret_cast<const uint4*>(&tl[(r * K + j) * kTabStride]);
-                t2 = tl[(r * K + j) * kTabStride + 4];
-            }
+            const uint4 tq = *reinterpret_cast<const uint4*>(&tl[(r * K + j) * kTabStride]);
+            const uint32_t t2 = tl[(r * K + j) * kTabStride + 4];
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
                 const uint32_t v = xor3(__builtin_amdgcn_perm(tq.y, tq.x, s0[w]),
@@ -409,12 +395,10 @@ __global__ __launch_bounds__(kBlock) void hash_reduce(const uint32_t* __restrict
 }
 
 // Small chunks (<= 4 KiB per shard) ran 3-4 % faster with 128-thread blocks,
-// and so did 4-row launches (RS(12,8) encode, +2-3.5 % in two sweeps).
-#ifdef AB_BLOCK128
-inline int block_for(uint64_t, int) { return 128; }
-#else
-inline int block_for(uint64_t len, int rows) { return (len <= 4096 || rows >= 4) ? 128 : kBlock; }
-#endif
+// and so did launches with >= 16 coefficients (RS(12,8) encode +2-3.5 %, decode
+// +1 %); RS(6,4) encode/decode lose 1-2 % with them (interleaved A/B runs).
+// Keeping the tables in SGPRs instead of LDS (no barrier) lost 1 % on RS(6,4).
+inline int block_for(uint64_t len, int coefs) { return (len <= 4096 || coefs >= 16) ? 128 : kBlock; }
 
 template <int K, int R, bool PAD>
 hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
@@ -435,7 +419,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     a.hbase = p.hash_base;
     for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(p.coef[(r0 + r) * p.cols + j]);
-    const int block = block_for(p.len, R);
+    const int block = block_for(p.len, R * K);
     const uint64_t per_launch = kMaxIndex / segs64;  // stripes per launch keeping idx < 2^31
     for (uint64_t s0 = 0; s0 < p.stripes; s0 += per_launch) {
         const uint64_t ns = std::min<uint64_t>(per_launch, p.stripes - s0);
