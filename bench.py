@@ -55,6 +55,8 @@ def parse():
                          "JNI-style synchronous host-memory encode at ELECT's codeLength")
     ap.add_argument("--threads", type=int, default=16, help="hostpath: concurrent callers")
     ap.add_argument("--batch", action="store_true", help="hostpath: cross-thread batching on")
+    ap.add_argument("--pad-fill", default="random",
+                    help="padded: content lengths 'random' (uniform [0, L]) or a fixed fraction of L")
     ap.add_argument("--host-chunk", type=int, default=4404020, help="hostpath: bytes per unit per call")
     return ap.parse_args()
 
@@ -392,7 +394,10 @@ def config_padded(args, world, rank, dev):
     k, m, L, B = 4, 2, 65536, 4096
     coder = RSCoder(k, m)
     data = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev)
-    lens = torch.randint(0, L + 1, (B, k), dtype=torch.int32, device=dev)
+    if args.pad_fill == "random":
+        lens = torch.randint(0, L + 1, (B, k), dtype=torch.int32, device=dev)
+    else:
+        lens = torch.full((B, k), int(float(args.pad_fill) * L), dtype=torch.int32, device=dev)
     par = torch.empty((B, m, L), dtype=torch.uint8, device=dev)
     evs = []
 
@@ -423,7 +428,8 @@ def config_padded(args, world, rank, dev):
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                          "kernel": "gf_apply_x16<4,2,padded>", "algorithmic_bytes_per_launch": alg,
                          "fill": round(valid / (B * k * L), 3)},
-            "config": {"workload": f"{B} stripes, content lengths uniform in [0, {L}]",
+            "config": {"workload": f"{B} stripes, content lengths " + (f"uniform in [0, {L}]" if args.pad_fill == "random"
+                                                                     else f"{args.pad_fill} x {L}"),
                        "parallelism": f"stripe-partitioned x{world}"}}
 
 

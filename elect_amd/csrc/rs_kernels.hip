@@ -233,6 +233,57 @@ struct FastArgs {
 
 constexpr int kTabStride = 8;  // dwords per coefficient in LDS
 
+// cmask (wave-uniform): columns to include; the others are known zero for the
+// whole wave and are skipped by a scalar branch (padded launches).
+template <int K, int R, bool MASKED = false>
+__device__ __forceinline__ void gf_combine(const uint4 (&x)[K], const uint32_t* tl, uint4 (&acc)[R],
+                                           uint32_t cmask = ~0u)
+{
+    if (MASKED) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {  // column-outer: selectors once, then every row
+        if (MASKED && !(cmask & (1u << j))) continue;
+        uint32_t s0[4], s1[4], s2[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const Sel sl = selectors(lane_word(x[j], w));
+            s0[w] = sl.s0;
+            s1[w] = sl.s1;
+            s2[w] = sl.s2;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint4 tq = *reinterpret_cast<const uint4*>(&tl[(r * K + j) * kTabStride]);
+            const uint32_t t2 = tl[(r * K + j) * kTabStride + 4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t v = xor3(__builtin_amdgcn_perm(tq.y, tq.x, s0[w]),
+                                        __builtin_amdgcn_perm(tq.w, tq.z, s1[w]),
+                                        __builtin_amdgcn_perm(t2, t2, s2[w]));
+                set_word(acc[r], w, (j == 0 && !MASKED) ? v : (lane_word(acc[r], w) ^ v));
+            }
+        }
+    }
+}
+
+// Stage the byte-shuffle tables of a launch into LDS (8 dwords per coefficient).
+template <int K, int R>
+__device__ __forceinline__ void stage_tables(const FastArgs<K, R>& a, uint32_t* tl)
+{
+    for (int i = threadIdx.x; i < R * K; i += blockDim.x) {
+        const gf::PermTable& t = a.tab[i / K][i % K];
+        tl[i * kTabStride + 0] = t.t0_lo;
+        tl[i * kTabStride + 1] = t.t0_hi;
+        tl[i * kTabStride + 2] = t.t1_lo;
+        tl[i * kTabStride + 3] = t.t1_hi;
+        tl[i * kTabStride + 4] = t.t2;
+    }
+    __syncthreads();
+}
+
 template <int K, int R, bool PAD>
 __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 {
@@ -259,15 +310,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         for (int j = 0; j < K; ++j) sl[j] = __builtin_amdgcn_readfirstlane(l[j]);
     }
 
-    for (int i = threadIdx.x; i < R * K; i += blockDim.x) {
-        const gf::PermTable& t = a.tab[i / K][i % K];
-        tl[i * kTabStride + 0] = t.t0_lo;
-        tl[i * kTabStride + 1] = t.t0_hi;
-        tl[i * kTabStride + 2] = t.t1_lo;
-        tl[i * kTabStride + 3] = t.t1_hi;
-        tl[i * kTabStride + 4] = t.t2;
-    }
-    __syncthreads();
+    stage_tables(a, tl);
     if (!live) return;
     if (!PAD) {
 #pragma unroll
@@ -305,29 +348,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
     }
 
     uint4 acc[R];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {  // column-outer: selectors once, then every row
-        uint32_t s0[4], s1[4], s2[4];
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const Sel sl = selectors(lane_word(x[j], w));
-            s0[w] = sl.s0;
-            s1[w] = sl.s1;
-            s2[w] = sl.s2;
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint4 tq = *reinterpret_cast<const uint4*>(&tl[(r * K + j) * kTabStride]);
-            const uint32_t t2 = tl[(r * K + j) * kTabStride + 4];
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const uint32_t v = xor3(__builtin_amdgcn_perm(tq.y, tq.x, s0[w]),
-                                        __builtin_amdgcn_perm(tq.w, tq.z, s1[w]),
-                                        __builtin_amdgcn_perm(t2, t2, s2[w]));
-                set_word(acc[r], w, j == 0 ? v : (lane_word(acc[r], w) ^ v));
-            }
-        }
-    }
+    gf_combine<K, R>(x, tl, acc);
     if (!PAD || off + 16 <= a.len) {
 #pragma unroll
         for (int r = 0; r < R; ++r) store_nt(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
@@ -372,6 +393,127 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         }
     }
 }
+
+// Padded launches with per-stripe content lengths, no hash, and L % 16 == 0:
+// U segments per lane.  The lengths sit on the critical path of every data
+// load (no load past a unit's content), so a wave amortises that dependent
+// round trip over U x 1 KiB per column instead of 1 KiB; a wave whose 64*U
+// segments lie in one stripe reads the lengths once, as scalar loads
+// overlapped with the table staging.  The one segment per unit that straddles
+// its content length is loaded whole (it lies inside the unit's L bytes) and
+// masked, so no byte loads.  Straddling waves take a one-segment-at-a-time path.
+__device__ __forceinline__ uint4 keep_bytes(const uint4& v, uint32_t n)  // bytes [0, n) of 16
+{
+    uint4 o;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t lo = 4 * w;
+        const uint32_t keep = n >= lo + 4 ? 0xFFFFFFFFu : n <= lo ? 0u : ((1u << (8 * (n - lo))) - 1u);
+        set_word(o, w, lane_word(v, w) & keep);
+    }
+    return o;
+}
+
+constexpr int kAuxNT = 2;  // buffer op cache policy: nt (gfx940 family CPol)
+
+template <int K, int R, int U>
+__global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t first = __builtin_amdgcn_readfirstlane(((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * (64u * U));
+    auto stripe_of = [&](uint32_t i) { return static_cast<uint32_t>((static_cast<uint64_t>(i) * a.magic) >> a.shift); };
+    bool uniform = false;
+    uint32_t s0 = 0, sl[K];
+    if (first < a.total) {
+        s0 = stripe_of(first);
+        uniform = s0 == stripe_of(min(first + 64u * U - 1u, a.total - 1u));
+        const uint32_t* l = a.lens + static_cast<uint64_t>(s0) * a.lstride;
+#pragma unroll
+        for (int j = 0; j < K; ++j) sl[j] = __builtin_amdgcn_readfirstlane(l[j]);
+    }
+    stage_tables(a, tl);
+    if (first >= a.total) return;
+
+    if (uniform) {
+        // One buffer descriptor per column whose range ends at the content
+        // length rounded up to the segment: the range check turns every load
+        // past it into zeros with no memory access, so all loads issue
+        // unconditionally, back to back.  The one straddling segment is masked.
+        __amdgpu_buffer_rsrc_t rs[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.sp[j] + s0 * a.ss[j]), 0,
+                                                      static_cast<int>((sl[j] + 15u) & ~15u), 0x00020000);
+        uint4 x[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t off = (first + u * 64u + lane - s0 * a.segs) * 16u;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs[j], static_cast<int>(off), 0, kAuxNT);
+                x[u][j] = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t off0 = (first + u * 64u - s0 * a.segs) * 16u;  // the wave's lowest offset
+            const uint32_t off = off0 + lane * 16u;
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                if (off0 < sl[j] && sl[j] < off0 + 1024u && (sl[j] & 15u))  // wave-uniform: this slice holds the content end
+                    x[u][j] = keep_bytes(x[u][j], off < sl[j] ? min(sl[j] - off, 16u) : 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t idx = first + u * 64u + lane;
+            if (idx >= a.total) break;
+            const uint64_t off = static_cast<uint64_t>(idx - s0 * a.segs) * 16;
+            // Skip the columns of empty units (ELECT's all-zero filler chunks).
+            // Skipping every column that is zero for this wave slice was 2-3 %
+            // slower at partial fills (interleaved A/B), though 45 % faster
+            // with every unit empty; empty units get the same gain.
+            uint32_t cmask = 0;
+#pragma unroll
+            for (int j = 0; j < K; ++j) cmask |= (sl[j] != 0 ? 1u : 0u) << j;
+            uint4 acc[R];
+            gf_combine<K, R, true>(x[u], tl, acc, cmask);
+#pragma unroll
+            for (int r = 0; r < R; ++r) store_nt(a.dp[r] + s0 * a.ds[r] + off, acc[r]);
+        }
+        return;
+    }
+    for (int u = 0; u < U; ++u) {  // straddling wave: per-lane stripes and lengths
+        const uint32_t idx = first + u * 64u + lane;
+        if (idx >= a.total) break;
+        const uint32_t stripe = stripe_of(idx);
+        const uint64_t off = static_cast<uint64_t>(idx - stripe * a.segs) * 16;
+        const uint32_t* l = a.lens + static_cast<uint64_t>(stripe) * a.lstride;
+        uint32_t valid[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) valid[j] = l[j];
+        uint4 x[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            x[j] = make_uint4(0, 0, 0, 0);
+            if (off < valid[j]) x[j] = load_nt(a.sp[j] + stripe * a.ss[j] + off);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if (off < valid[j] && off + 16 > valid[j]) x[j] = keep_bytes(x[j], static_cast<uint32_t>(valid[j] - off));
+        uint4 acc[R];
+        gf_combine<K, R>(x, tl, acc);
+#pragma unroll
+        for (int r = 0; r < R; ++r) store_nt(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
+    }
+}
+
+#ifndef AB_PAD_U4
+#define AB_PAD_U4 4
+#endif
+// Segments per lane for gf_apply_lens: U*K 16-byte loads in flight per lane.
+template <int K>
+constexpr int lens_unroll() { return K <= 4 ? AB_PAD_U4 : 1; }
 
 // Sum the per-wave hash partials of each (stripe, row): the waves lying wholly
 // inside stripe s are [ceil(s*segs/64), floor((s+1)*segs/64)); straddling waves
@@ -440,8 +582,20 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             const hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&a.hpart), bytes, stream);
             if (e != hipSuccess) return e;
         }
-        const uint32_t grid = (a.total + block - 1) / block;
-        hipLaunchKernelGGL((gf_apply_x16<K, R, PAD>), dim3(grid), dim3(block), 0, stream, a);
+        bool lens_path = false;
+        if constexpr (PAD) {
+            lens_path = a.lens && !a.hashes && p.len % 16 == 0 && p.len < (uint64_t{1} << 31);
+            if (lens_path) {
+                constexpr int U = lens_unroll<K>();
+                const uint64_t threads = (static_cast<uint64_t>(a.total) + 64 * U - 1) / (64 * U) * 64;
+                hipLaunchKernelGGL((gf_apply_lens<K, R, U>), dim3(static_cast<uint32_t>((threads + block - 1) / block)),
+                                   dim3(block), 0, stream, a);
+            }
+        }
+        if (!lens_path) {
+            const uint32_t grid = (a.total + block - 1) / block;
+            hipLaunchKernelGGL((gf_apply_x16<K, R, PAD>), dim3(grid), dim3(block), 0, stream, a);
+        }
         hipError_t e = hipGetLastError();
         if (e == hipSuccess && a.hashes) {
             const uint32_t n = static_cast<uint32_t>(ns) * R;  // one wave each

@@ -167,7 +167,8 @@ int elect_ec_decode_batch(const elect_ec_coder* coder, size_t chunk_size, size_t
                           unsigned flags, int mode, void* stream);
 /* Zero-padded batch encode: data_lengths is a DEVICE array [num_stripes][k] of
  * uint32 content lengths (each <= chunk_size); bytes past a unit's length read
- * as zero and are never loaded. */
+ * as zero whatever the buffer holds there.  Loads stop at the 16-byte segment
+ * holding a unit's last content byte (always inside its chunk_size bytes). */
 int elect_ec_encode_batch_padded(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
                                  elect_ec_shards data, const uint32_t* data_lengths,
                                  elect_ec_shards parity, void* stream);

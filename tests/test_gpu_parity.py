@@ -252,12 +252,16 @@ def _zero_padded(data, lens):
     return out
 
 
-@pytest.mark.parametrize("k,m,L", [(4, 2, 65536), (4, 2, 4099), (8, 4, 1000), (3, 2, 17), (10, 4, 333)])
+@pytest.mark.parametrize("k,m,L", [(4, 2, 65536), (4, 2, 4099), (8, 4, 1000), (3, 2, 17), (10, 4, 333),
+                                   (4, 2, 1040), (4, 2, 16), (2, 1, 4096 + 48), (8, 4, 2048), (5, 3, 1056),
+                                   (10, 4, 4096)])
 def test_encode_batch_padded_ignores_bytes_past_length(dev, oracle, k, m, L):
     """ELECT zero-fills each SSTable to codeLength (ECMessageVerbHandler.java:292-310)
     and pads missing primaries with all-zero chunks (:174-184).  The padded kernel
-    must give the parity of the zero-padded stripe while never reading past each
-    content length: the buffers hold 0xFF garbage there."""
+    must give the parity of the zero-padded stripe whatever the bytes past each
+    content length hold: the buffers hold 0xFF garbage there.  L % 16 == 0 cases
+    take gf_apply_lens (U segments per lane; L = 1040 makes its waves straddle
+    stripes), the others gf_apply_x16<PAD>."""
     from elect_amd.batch import encode_batch_padded
     from elect_amd.coder import RSCoder
     rng = np.random.default_rng(L * 3 + k)

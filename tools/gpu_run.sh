@@ -69,9 +69,14 @@ for step in "$@"; do
         for i in 1 2 3; do for v in a ${AB_VARIANTS:-b}; do
             lib=""; [ $v = a ] || lib="$PWD/elect_amd/_ab/libelect_ec_$v.so"
             for c in ${AB_CONFIGS:-headline rs12 padded}; do
-                ELECT_EC_LIB=$lib run "ab_${v}_${c}_$i" 300 python bench.py --config $c --no-cpu --no-host --steps 50 || exit $?
+                cfg=${c%%:*}; extra=""; [ "$cfg" != "$c" ] && extra="--pad-fill ${c#*:}"
+                ELECT_EC_LIB=$lib run "ab_${v}_${c/:/-}_$i" 300 python bench.py --config $cfg $extra --no-cpu --no-host --steps 50 || exit $?
             done
         done; done ;;
+    padfill)  # padded encode vs content fill: where the time goes
+        for f in 1.0 0.0 0.5 random; do
+            run "bench_padded_fill_$f" 300 python bench.py --config padded --pad-fill $f || exit $?
+        done ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
