@@ -54,8 +54,10 @@ static jfieldID coder_field(JNIEnv* env, jobject thiz)
 {
     jclass clazz = (*env)->GetObjectClass(env, thiz);
     jfieldID fid = (*env)->GetFieldID(env, clazz, "nativeCoder", "J");
-    if (fid == NULL)
+    if (fid == NULL) {  /* GetFieldID left NoSuchFieldError pending; report it as the reference does */
+        (*env)->ExceptionClear(env);
         throw_java(env, "java/lang/UnsatisfiedLinkError", "Field nativeCoder not found");
+    }
     return fid;
 }
 
@@ -115,14 +117,22 @@ static int buffers(JNIEnv* env, jobjectArray arr, jintArray offsets, int num, un
     return 0;
 }
 
+/* initImpl (EC/NativeRSEncoder.c:31-41, EC/NativeRSDecoder.c:32-42): the field
+ * is resolved first, so a class without it leaks no coder. */
+static void init_coder(JNIEnv* env, jobject thiz, jint k, jint m)
+{
+    jfieldID fid = coder_field(env, thiz);
+    elect_ec_coder* c = NULL;
+    if (fid == NULL || raise_status(env, elect_ec_coder_create(k, m, &c), "initImpl"))
+        return;
+    (*env)->SetLongField(env, thiz, fid, (jlong)(intptr_t)c);
+}
+
 JNIEXPORT void JNICALL
 Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_initImpl(JNIEnv* env, jobject thiz,
                                                                   jint numDataUnits, jint numParityUnits)
 {
-    elect_ec_coder* c = NULL;
-    if (raise_status(env, elect_ec_coder_create(numDataUnits, numParityUnits, &c), "initImpl"))
-        return;
-    set_coder(env, thiz, c);
+    init_coder(env, thiz, numDataUnits, numParityUnits);
 }
 
 JNIEXPORT void JNICALL
@@ -184,10 +194,7 @@ JNIEXPORT void JNICALL
 Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_initImpl(JNIEnv* env, jobject thiz,
                                                                   jint numDataUnits, jint numParityUnits)
 {
-    elect_ec_coder* c = NULL;
-    if (raise_status(env, elect_ec_coder_create(numDataUnits, numParityUnits, &c), "initImpl"))
-        return;
-    set_coder(env, thiz, c);
+    init_coder(env, thiz, numDataUnits, numParityUnits);
 }
 
 /* ELECT_EC_DECODE_MODE=strict switches off the compat zero rows for every

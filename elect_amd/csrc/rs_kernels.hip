@@ -540,7 +540,11 @@ __global__ __launch_bounds__(kBlock) void hash_reduce(const uint32_t* __restrict
 // and so did launches with >= 16 coefficients (RS(12,8) encode +2-3.5 %, decode
 // +1 %); RS(6,4) encode/decode lose 1-2 % with them (interleaved A/B runs).
 // Keeping the tables in SGPRs instead of LDS (no barrier) lost 1 % on RS(6,4).
+#ifdef AB_BLOCK  // A/B builds (tools/ab_build.sh): one block size for every launch
+inline int block_for(uint64_t, int) { return AB_BLOCK; }
+#else
 inline int block_for(uint64_t len, int coefs) { return (len <= 4096 || coefs >= 16) ? 128 : kBlock; }
+#endif
 
 template <int K, int R, bool PAD>
 hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)

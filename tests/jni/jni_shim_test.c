@@ -1,0 +1,545 @@
+/*
+ * jni_shim_test.c — a fake JVM that loads the drop-in libec shim the way
+ * System.loadLibrary("ec") does (dlopen + dlsym of the seven
+ * Java_org_apache_cassandra_io_erasurecode_* names, JEC/NativeRSEncoder.java:97-105,
+ * JEC/NativeRSDecoder.java:81-87) and calls them with Java-shaped arguments:
+ * ByteBuffer[] arrays, int[] position offsets, a `long nativeCoder` field.
+ *
+ *   jni_shim_test LIB cpu          error paths; no device needed (exit 0 = pass)
+ *   jni_shim_test LIB gpu OUTDIR   ErasureCodeTest.java:31-173 at codeLength 4099
+ *                                  through the JNI entry points, buffers at
+ *                                  non-zero positions; writes them to OUTDIR for
+ *                                  the Python side to compare with
+ *                                  tests/golden/erasure_code_test.json
+ *
+ * The fake JVM also enforces JNI rules the reference glue breaks
+ * (EC/jni_common.c:70-75, EC/NativeRSDecoder.c:50-62): no JNI call other than
+ * the exception-safe ones while an exception is pending, every
+ * Get<Int>ArrayElements released, every local ref from GetObjectArrayElement
+ * deleted.  Built against tests/jni/mock/jni.h (test double; see its header).
+ */
+#include <dlfcn.h>
+#include <jni.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ENC_CLS "org/apache/cassandra/io/erasurecode/NativeRSEncoder"
+#define DEC_CLS "org/apache/cassandra/io/erasurecode/NativeRSDecoder"
+
+enum { K_CLASS, K_OBJECT, K_DIRECT, K_HEAP, K_OBJARR, K_INTARR };
+
+struct _jobject {
+    int kind;
+    const char* cls;
+    jlong native_coder;
+    jboolean verbose;
+    unsigned char* addr;
+    jobject* elems;
+    jint* ints;
+    int n;
+};
+
+static struct {
+    int pending;
+    char exc_class[128];
+    char exc_msg[256];
+    int violations;
+    int live_int_elems;
+    int local_refs;
+} vm;
+
+static int failures;
+#define EXPECT(cond)                                                                   \
+    do {                                                                               \
+        if (!(cond)) {                                                                 \
+            fprintf(stderr, "FAIL %s:%d %s\n", __FILE__, __LINE__, #cond);             \
+            ++failures;                                                                \
+        }                                                                              \
+    } while (0)
+
+static void no_pending(const char* fn)
+{
+    if (vm.pending) {
+        fprintf(stderr, "JNI violation: %s called with %s pending\n", fn, vm.exc_class);
+        ++vm.violations;
+    }
+}
+
+static void raise_exc(const char* cls, const char* msg)
+{
+    if (vm.pending) return;  /* the first exception wins, as in the JVM */
+    vm.pending = 1;
+    snprintf(vm.exc_class, sizeof vm.exc_class, "%s", cls);
+    snprintf(vm.exc_msg, sizeof vm.exc_msg, "%s", msg ? msg : "");
+}
+
+static jobject new_obj(int kind, const char* cls)
+{
+    jobject o = calloc(1, sizeof *o);
+    o->kind = kind;
+    o->cls = cls;
+    return o;
+}
+
+/* ---- the JNIEnv functions the shim uses ---------------------------------- */
+static jclass m_FindClass(JNIEnv* env, const char* name)
+{
+    (void)env;
+    no_pending("FindClass");
+    return new_obj(K_CLASS, strdup(name));
+}
+
+static jint m_ThrowNew(JNIEnv* env, jclass c, const char* msg)
+{
+    (void)env;
+    no_pending("ThrowNew");
+    raise_exc(c->cls, msg);
+    return 0;
+}
+
+static void m_ExceptionClear(JNIEnv* env)
+{
+    (void)env;
+    vm.pending = 0;
+}
+
+static jclass m_GetObjectClass(JNIEnv* env, jobject o)
+{
+    (void)env;
+    no_pending("GetObjectClass");
+    return new_obj(K_CLASS, o->cls);
+}
+
+static int is_coder_class(jclass c) { return !strcmp(c->cls, ENC_CLS) || !strcmp(c->cls, DEC_CLS); }
+
+static jfieldID m_GetFieldID(JNIEnv* env, jclass c, const char* name, const char* sig)
+{
+    (void)env;
+    no_pending("GetFieldID");
+    if (is_coder_class(c) && !strcmp(name, "nativeCoder") && !strcmp(sig, "J"))
+        return (jfieldID)1;
+    raise_exc("java/lang/NoSuchFieldError", name);
+    return NULL;
+}
+
+static jmethodID m_GetMethodID(JNIEnv* env, jclass c, const char* name, const char* sig)
+{
+    (void)env;
+    no_pending("GetMethodID");
+    if (is_coder_class(c) && !strcmp(name, "allowVerboseDump") && !strcmp(sig, "()Z"))
+        return (jmethodID)2;
+    raise_exc("java/lang/NoSuchMethodError", name);
+    return NULL;
+}
+
+static jboolean m_CallBooleanMethod(JNIEnv* env, jobject o, jmethodID mid, ...)
+{
+    (void)env;
+    no_pending("CallBooleanMethod");
+    return mid == (jmethodID)2 ? o->verbose : JNI_FALSE;
+}
+
+static jlong m_GetLongField(JNIEnv* env, jobject o, jfieldID f)
+{
+    (void)env;
+    (void)f;
+    no_pending("GetLongField");
+    return o->native_coder;
+}
+
+static void m_SetLongField(JNIEnv* env, jobject o, jfieldID f, jlong v)
+{
+    (void)env;
+    (void)f;
+    no_pending("SetLongField");
+    o->native_coder = v;
+}
+
+static jsize m_GetArrayLength(JNIEnv* env, jarray a)
+{
+    (void)env;
+    no_pending("GetArrayLength");
+    return a->n;
+}
+
+static jobject m_GetObjectArrayElement(JNIEnv* env, jobjectArray a, jsize i)
+{
+    (void)env;
+    no_pending("GetObjectArrayElement");
+    if (i < 0 || i >= a->n) {
+        raise_exc("java/lang/ArrayIndexOutOfBoundsException", "");
+        return NULL;
+    }
+    if (a->elems[i]) ++vm.local_refs;
+    return a->elems[i];
+}
+
+static jint* m_GetIntArrayElements(JNIEnv* env, jintArray a, jboolean* is_copy)
+{
+    (void)env;
+    no_pending("GetIntArrayElements");
+    jint* p = malloc(sizeof(jint) * (a->n ? a->n : 1));
+    memcpy(p, a->ints, sizeof(jint) * a->n);
+    if (is_copy) *is_copy = JNI_TRUE;
+    ++vm.live_int_elems;
+    return p;
+}
+
+static void m_ReleaseIntArrayElements(JNIEnv* env, jintArray a, jint* p, jint mode)
+{
+    (void)env;  /* exception-safe per the JNI spec */
+    if (mode != JNI_ABORT) memcpy(a->ints, p, sizeof(jint) * a->n);
+    free(p);
+    --vm.live_int_elems;
+}
+
+static void m_GetIntArrayRegion(JNIEnv* env, jintArray a, jsize start, jsize len, jint* buf)
+{
+    (void)env;
+    no_pending("GetIntArrayRegion");
+    if (start < 0 || len < 0 || start + len > a->n) {
+        raise_exc("java/lang/ArrayIndexOutOfBoundsException", "");
+        return;
+    }
+    memcpy(buf, a->ints + start, sizeof(jint) * len);
+}
+
+static void* m_GetDirectBufferAddress(JNIEnv* env, jobject o)
+{
+    (void)env;
+    no_pending("GetDirectBufferAddress");
+    return o->kind == K_DIRECT ? o->addr : NULL;
+}
+
+static void m_DeleteLocalRef(JNIEnv* env, jobject o)
+{
+    (void)env;  /* exception-safe per the JNI spec */
+    if (o) --vm.local_refs;
+}
+
+static const struct JNINativeInterface_ kEnvTable = {
+    m_FindClass,         m_ThrowNew,           m_ExceptionClear,        m_GetObjectClass,
+    m_GetFieldID,        m_GetMethodID,        m_CallBooleanMethod,     m_GetLongField,
+    m_SetLongField,      m_GetArrayLength,     m_GetObjectArrayElement, m_GetIntArrayElements,
+    m_ReleaseIntArrayElements, m_GetIntArrayRegion, m_GetDirectBufferAddress, m_DeleteLocalRef,
+};
+static JNIEnv kEnv = &kEnvTable;
+static JNIEnv* env = &kEnv;
+
+/* ---- the seven native methods, resolved by name like the JVM does --------- */
+typedef void (*init_fn)(JNIEnv*, jobject, jint, jint);
+typedef void (*encode_fn)(JNIEnv*, jobject, jobjectArray, jintArray, jint, jobjectArray, jintArray);
+typedef void (*update_fn)(JNIEnv*, jobject, jobjectArray, jintArray, jint, jint, jobjectArray, jintArray);
+typedef void (*destroy_fn)(JNIEnv*, jobject);
+typedef void (*decode_fn)(JNIEnv*, jobject, jobjectArray, jintArray, jint, jintArray, jintArray, jobjectArray,
+                          jintArray);
+
+static struct {
+    init_fn enc_init, dec_init;
+    encode_fn encode;
+    update_fn update;
+    decode_fn decode;
+    destroy_fn enc_destroy, dec_destroy;
+    int (*device_count)(int*);
+} jni;
+
+static void* sym(void* h, const char* name)
+{
+    void* p = dlsym(h, name);
+    if (!p) {
+        fprintf(stderr, "missing symbol %s\n", name);
+        exit(2);
+    }
+    return p;
+}
+
+#define PFX "Java_org_apache_cassandra_io_erasurecode_"
+static void load(const char* lib)
+{
+    void* h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+        fprintf(stderr, "dlopen %s: %s\n", lib, dlerror());
+        exit(2);
+    }
+    jni.enc_init = (init_fn)sym(h, PFX "NativeRSEncoder_initImpl");
+    jni.encode = (encode_fn)sym(h, PFX "NativeRSEncoder_encodeImpl");
+    jni.update = (update_fn)sym(h, PFX "NativeRSEncoder_encodeUpdateImpl");
+    jni.enc_destroy = (destroy_fn)sym(h, PFX "NativeRSEncoder_destroyImpl");
+    jni.dec_init = (init_fn)sym(h, PFX "NativeRSDecoder_initImpl");
+    jni.decode = (decode_fn)sym(h, PFX "NativeRSDecoder_decodeImpl");
+    jni.dec_destroy = (destroy_fn)sym(h, PFX "NativeRSDecoder_destroyImpl");
+    jni.device_count = (int (*)(int*))sym(h, "elect_ec_device_count");
+}
+
+/* ---- Java-side object builders ------------------------------------------- */
+static jobject coder_obj(const char* cls) { return new_obj(K_OBJECT, cls); }
+
+static jobject direct_bb(unsigned char* base)
+{
+    jobject o = new_obj(K_DIRECT, "java/nio/DirectByteBuffer");
+    o->addr = base;
+    return o;
+}
+
+static jobject obj_array(int n, const jobject* e)
+{
+    jobject a = new_obj(K_OBJARR, "[Ljava/nio/ByteBuffer;");
+    a->n = n;
+    a->elems = calloc(n ? n : 1, sizeof(jobject));
+    if (n) memcpy(a->elems, e, sizeof(jobject) * n);
+    return a;
+}
+
+static jobject int_array(int n, const jint* v)
+{
+    jobject a = new_obj(K_INTARR, "[I");
+    a->n = n;
+    a->ints = calloc(n ? n : 1, sizeof(jint));
+    if (n) memcpy(a->ints, v, sizeof(jint) * n);
+    return a;
+}
+
+/* Expect exactly the Java exception `cls` (message containing `needle`), then clear it. */
+static int threw(const char* cls, const char* needle)
+{
+    const int ok = vm.pending && !strcmp(vm.exc_class, cls) && (!needle || strstr(vm.exc_msg, needle));
+    if (!ok)
+        fprintf(stderr, "  expected %s(%s), got %s(%s)\n", cls, needle ? needle : "", vm.pending ? vm.exc_class : "none",
+                vm.pending ? vm.exc_msg : "");
+    vm.pending = 0;
+    return ok;
+}
+
+static int clean(void)
+{
+    if (vm.pending) fprintf(stderr, "  unexpected %s(%s)\n", vm.exc_class, vm.exc_msg);
+    const int ok = !vm.pending;
+    vm.pending = 0;
+    return ok;
+}
+
+/* n direct buffers of len bytes at position pos[i] inside their backing memory */
+struct Bufs {
+    int n;
+    unsigned char* mem[16];
+    jobject bb[16];
+    jint pos[16];
+};
+
+static void bufs_init(struct Bufs* b, int n, size_t len, int pos0)
+{
+    b->n = n;
+    for (int i = 0; i < n; ++i) {
+        b->pos[i] = pos0 + 3 * i;
+        b->mem[i] = calloc(len + b->pos[i] + 16, 1);
+        b->bb[i] = direct_bb(b->mem[i]);
+    }
+}
+
+static unsigned char* at(struct Bufs* b, int i) { return b->mem[i] + b->pos[i]; }
+
+/* ---- cpu: error behaviour ------------------------------------------------- */
+static int cpu_checks(void)
+{
+    jobject enc = coder_obj(ENC_CLS), dec = coder_obj(DEC_CLS);
+    struct Bufs d, p;
+    bufs_init(&d, 4, 16, 1);
+    bufs_init(&p, 2, 16, 2);
+
+    jni.enc_init(env, enc, 0, 2);  /* invalid k: no coder, Java sees an exception */
+    EXPECT(threw("java/lang/IllegalArgumentException", "invalid argument"));
+    EXPECT(enc->native_coder == 0);
+
+    jni.enc_init(env, enc, 4, 2);
+    EXPECT(clean());
+    EXPECT(enc->native_coder != 0);
+
+    /* count mismatch -> InternalError "Invalid inputs" (EC/jni_common.c:70-73) */
+    jobject in3 = obj_array(3, d.bb), off3 = int_array(3, d.pos);
+    jobject in4 = obj_array(4, d.bb), off4 = int_array(4, d.pos);
+    jobject out2 = obj_array(2, p.bb), poff2 = int_array(2, p.pos);
+    jni.encode(env, enc, in3, off3, 16, out2, poff2);
+    EXPECT(threw("java/lang/InternalError", "Invalid inputs"));
+    jobject out1 = obj_array(1, p.bb), poff1 = int_array(1, p.pos);
+    jni.encode(env, enc, in4, off4, 16, out1, poff1);
+    EXPECT(threw("java/lang/InternalError", "Invalid outputs"));
+
+    /* a heap ByteBuffer has no direct address -> InternalError */
+    jobject heap[4] = {d.bb[0], d.bb[1], new_obj(K_HEAP, "java/nio/HeapByteBuffer"), d.bb[3]};
+    jobject inh = obj_array(4, heap);
+    jni.encode(env, enc, inh, off4, 16, out2, poff2);
+    EXPECT(threw("java/lang/InternalError", "Invalid inputs"));
+
+    /* a null element -> InternalError */
+    jobject nul[4] = {d.bb[0], NULL, d.bb[2], d.bb[3]};
+    jni.encode(env, enc, obj_array(4, nul), off4, 16, out2, poff2);
+    EXPECT(threw("java/lang/InternalError", "Invalid inputs"));
+
+    /* encodeUpdate takes [old, new, P0..m-1]: m + 2 inputs */
+    jni.update(env, enc, in3, off3, 16, 0, out2, poff2);
+    EXPECT(threw("java/lang/InternalError", "Invalid inputs"));
+
+    int ndev = 0;
+    if (jni.device_count(&ndev) != 0 || ndev == 0) {  /* no device: compute fails loudly */
+        jni.encode(env, enc, in4, off4, 16, out2, poff2);
+        EXPECT(threw("java/io/IOException", "no HIP device"));
+    }
+
+    /* destroy zeroes the field; use after destroy -> IOException (EC/NativeRSEncoder.c:46-50) */
+    jni.enc_destroy(env, enc);
+    EXPECT(clean());
+    EXPECT(enc->native_coder == 0);
+    jni.enc_destroy(env, enc);  /* idempotent */
+    EXPECT(clean());
+    jni.encode(env, enc, in4, off4, 16, out2, poff2);
+    EXPECT(threw("java/io/IOException", "NativeRSRawEncoder closed"));
+    jni.update(env, enc, in4, off4, 16, 0, out2, poff2);
+    EXPECT(threw("java/io/IOException", "NativeRSRawEncoder closed"));
+
+    /* decoder */
+    jni.dec_init(env, dec, 4, 2);
+    EXPECT(clean());
+    EXPECT(dec->native_coder != 0);
+    const jint di3[3] = {1, 2, 3}, di4[4] = {4, 1, 2, 3}, er1[1] = {0};
+    jni.decode(env, dec, in4, off4, 16, int_array(3, di3), int_array(1, er1), out1, poff1);
+    EXPECT(threw("java/lang/InternalError", "Invalid decode/erased indexes"));
+    jni.decode(env, dec, in3, off3, 16, int_array(4, di4), int_array(1, er1), out1, poff1);
+    EXPECT(threw("java/lang/InternalError", "Invalid inputs"));
+    jni.decode(env, dec, in4, off4, 16, int_array(4, di4), int_array(1, er1), out2, poff2);
+    EXPECT(threw("java/lang/InternalError", "Invalid outputs"));
+    const jint er_bad[1] = {7};  /* engine-side validation (unit 7 of 6) surfaces as a Java exception */
+    jni.decode(env, dec, in4, off4, 16, int_array(4, di4), int_array(1, er_bad), out1, poff1);
+    EXPECT(threw("java/lang/IllegalArgumentException", "invalid argument"));
+
+    /* an object without the nativeCoder field -> UnsatisfiedLinkError (EC/jni_common.h:29-36) */
+    jobject alien = coder_obj("java/lang/Object");
+    jni.enc_init(env, alien, 4, 2);
+    EXPECT(threw("java/lang/UnsatisfiedLinkError", "nativeCoder"));
+
+    jni.dec_destroy(env, dec);
+    EXPECT(clean());
+    EXPECT(dec->native_coder == 0);
+    jni.decode(env, dec, in4, off4, 16, int_array(4, di4), int_array(1, er1), out1, poff1);
+    EXPECT(threw("java/io/IOException", "NativeRSRawDecoder closed"));
+
+    EXPECT(vm.violations == 0);
+    EXPECT(vm.live_int_elems == 0);
+    EXPECT(vm.local_refs == 0);
+    return failures;
+}
+
+/* ---- gpu: ErasureCodeTest.java through the JNI entry points --------------- */
+typedef struct {
+    uint64_t seed;
+} JavaRandom;
+
+static void jr_init(JavaRandom* r, int64_t s) { r->seed = ((uint64_t)s ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1); }
+
+static void jr_next_bytes(JavaRandom* r, unsigned char* b, size_t n)
+{
+    for (size_t i = 0; i < n;) {
+        r->seed = (r->seed * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+        uint32_t v = (uint32_t)(int32_t)(r->seed >> 16);
+        for (int k = 0; k < 4 && i < n; ++k, v >>= 8) b[i++] = (unsigned char)v;
+    }
+}
+
+static void dump(const char* dir, const char* name, int idx, const unsigned char* p, size_t n)
+{
+    char path[1024];
+    snprintf(path, sizeof path, "%s/%s%d", dir, name, idx);
+    FILE* f = fopen(path, "wb");
+    if (!f || fwrite(p, 1, n, f) != n) {
+        fprintf(stderr, "cannot write %s\n", path);
+        exit(2);
+    }
+    fclose(f);
+}
+
+static int gpu_erasure_code_test(const char* outdir)
+{
+    enum { K = 4, M = 2 };
+    const jint L = 4099;
+    JavaRandom rnd;
+    jr_init(&rnd, 123);
+    struct Bufs data, modified, parity, second, upd, out1, out2;
+    bufs_init(&data, K, L, 1);
+    bufs_init(&modified, K, L, 2);
+    bufs_init(&parity, M, L, 5);
+    bufs_init(&second, M, L, 7);
+    bufs_init(&upd, M, L, 11);
+    bufs_init(&out1, 1, L, 13);
+    bufs_init(&out2, 1, L, 17);
+    for (int i = 0; i < K; ++i) {
+        jr_next_bytes(&rnd, at(&data, i), L);
+        memcpy(at(&modified, i), at(&data, i), L);
+    }
+    jr_next_bytes(&rnd, at(&modified, 0), L);
+
+    jobject enc = coder_obj(ENC_CLS), dec = coder_obj(DEC_CLS);
+    dec->verbose = JNI_TRUE;  /* exercise the allowVerboseDump() path */
+    jni.enc_init(env, enc, K, M);
+    jni.dec_init(env, dec, K, M);
+    EXPECT(clean());
+
+    jni.encode(env, enc, obj_array(K, data.bb), int_array(K, data.pos), L, obj_array(M, parity.bb),
+               int_array(M, parity.pos));
+    EXPECT(clean());
+    jni.encode(env, enc, obj_array(K, modified.bb), int_array(K, modified.pos), L, obj_array(M, second.bb),
+               int_array(M, second.pos));
+    EXPECT(clean());
+
+    const jint di[K] = {4, 1, 2, 3}, er[1] = {0};
+    jobject in1[K] = {parity.bb[0], data.bb[1], data.bb[2], data.bb[3]};
+    jint in1_pos[K] = {parity.pos[0], data.pos[1], data.pos[2], data.pos[3]};
+    jni.decode(env, dec, obj_array(K, in1), int_array(K, in1_pos), L, int_array(K, di), int_array(1, er),
+               obj_array(1, out1.bb), int_array(1, out1.pos));
+    EXPECT(clean());
+    jobject in2[K] = {second.bb[0], modified.bb[1], modified.bb[2], modified.bb[3]};
+    jint in2_pos[K] = {second.pos[0], modified.pos[1], modified.pos[2], modified.pos[3]};
+    jni.decode(env, dec, obj_array(K, in2), int_array(K, in2_pos), L, int_array(K, di), int_array(1, er),
+               obj_array(1, out2.bb), int_array(1, out2.pos));
+    EXPECT(clean());
+
+    jobject uin[2 + M] = {data.bb[0], modified.bb[0], parity.bb[0], parity.bb[1]};
+    jint uin_pos[2 + M] = {data.pos[0], modified.pos[0], parity.pos[0], parity.pos[1]};
+    jni.update(env, enc, obj_array(2 + M, uin), int_array(2 + M, uin_pos), L, 0, obj_array(M, upd.bb),
+               int_array(M, upd.pos));
+    EXPECT(clean());
+
+    EXPECT(!memcmp(at(&out1, 0), at(&data, 0), L));       /* ErasureCodeTest.java:112 */
+    EXPECT(!memcmp(at(&out2, 0), at(&modified, 0), L));   /* :119 */
+    for (int r = 0; r < M; ++r) EXPECT(!memcmp(at(&upd, r), at(&second, r), L));
+    /* bytes before each position are untouched */
+    for (int r = 0; r < M; ++r)
+        for (int b = 0; b < parity.pos[r]; ++b) EXPECT(parity.mem[r][b] == 0);
+
+    for (int i = 0; i < K; ++i) dump(outdir, "data", i, at(&data, i), L);
+    for (int r = 0; r < M; ++r) {
+        dump(outdir, "parity", r, at(&parity, r), L);
+        dump(outdir, "second", r, at(&second, r), L);
+        dump(outdir, "update", r, at(&upd, r), L);
+    }
+    jni.enc_destroy(env, enc);
+    jni.dec_destroy(env, dec);
+    EXPECT(enc->native_coder == 0 && dec->native_coder == 0);
+    EXPECT(vm.violations == 0);
+    EXPECT(vm.live_int_elems == 0);
+    EXPECT(vm.local_refs == 0);
+    return failures;
+}
+
+int main(int argc, char** argv)
+{
+    if (argc < 3) {
+        fprintf(stderr, "usage: %s LIB cpu | LIB gpu OUTDIR\n", argv[0]);
+        return 2;
+    }
+    load(argv[1]);
+    const int gpu = !strcmp(argv[2], "gpu");
+    const int rc = gpu ? gpu_erasure_code_test(argc > 3 ? argv[3] : ".") : cpu_checks();
+    printf("%s: %d failure(s), %d JNI violation(s)\n", argv[2], rc, vm.violations);
+    return rc == 0 ? 0 : 1;
+}

@@ -126,3 +126,19 @@ def test_cpp_mirror_erasure_code_test_on_gpu(dev, tmp_path):
     assert [digest(rd(f"parity{r}")) for r in range(2)] == g["parity"]
     assert [digest(rd(f"second{r}")) for r in range(2)] == g["second_parity"]
     assert [digest(rd(f"update{r}")) for r in range(2)] == g["update_parity"]
+
+
+def test_jni_shim_erasure_code_test_on_gpu(dev, tmp_path):
+    """ErasureCodeTest.java through the seven JNI entry points of the drop-in
+    libec.so shim (fake JVM, buffers at non-zero positions), on the GPU."""
+    import subprocess
+    from tests.jni_build import build
+    lib, drv = build()
+    r = subprocess.run([drv, lib, "gpu", str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    g = load("erasure_code_test.json")
+    rd = lambda n: np.fromfile(tmp_path / n, dtype=np.uint8)  # noqa: E731
+    assert [digest(rd(f"data{i}")) for i in range(4)] == g["data"]
+    assert [digest(rd(f"parity{r}")) for r in range(2)] == g["parity"]
+    assert [digest(rd(f"second{r}")) for r in range(2)] == g["second_parity"]
+    assert [digest(rd(f"update{r}")) for r in range(2)] == g["update_parity"]
