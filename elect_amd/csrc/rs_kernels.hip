@@ -165,6 +165,33 @@ __device__ __forceinline__ uint32_t horner31(const uint4& v)
     return h;
 }
 
+// 31^(16*seg) for a 32-bit segment index seg, from four 256-entry tables
+// (31^(16 * j * 256^i)): four scalar loads and three multiplies instead of a
+// square-and-multiply loop in the wave's epilogue.
+struct SegPow {
+    uint32_t t[4][256];
+    constexpr SegPow() : t()
+    {
+        uint32_t base = 1;
+        for (int i = 0; i < 16; ++i) base *= 31u;  // 31^16
+        for (int i = 0; i < 4; ++i) {
+            uint32_t x = 1;
+            for (int j = 0; j < 256; ++j) {
+                t[i][j] = x;
+                x *= base;
+            }
+            base = x;  // base^256
+        }
+    }
+};
+__constant__ constexpr SegPow kSegPow{};
+
+__device__ __forceinline__ uint32_t pow31_seg(uint32_t seg)
+{
+    return kSegPow.t[0][seg & 255u] * kSegPow.t[1][(seg >> 8) & 255u] * kSegPow.t[2][(seg >> 16) & 255u] *
+           kSegPow.t[3][seg >> 24];
+}
+
 // 31^(16*lane) for lane 0..63, a compile-time table (constant memory).
 struct LanePow {
     uint32_t v[64];
@@ -226,7 +253,7 @@ struct FastArgs {
     uint32_t clen[K];
     int32_t* hashes;        // optional parity hashes, [stripe][hstride] (row r at +r)
     uint32_t hstride;
-    uint64_t hbase;
+    uint32_t hpow;          // 31^(hash offset of byte 0 of this launch window)
     uint32_t* hpart;        // per-wave partial sums [wave][R] (waves wholly inside one stripe)
     gf::PermTable tab[R][K];
 };
@@ -377,7 +404,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         const bool whole_wave = last < a.total && s_first == s_last;  // wave-uniform
         if (whole_wave) {  // partial sums to scratch; hash_reduce adds them per stripe
             const uint32_t seg0 = first - s_first * a.segs;
-            const uint32_t p0 = dpow31(a.hbase + static_cast<uint64_t>(seg0) * 16);
+            const uint32_t p0 = a.hpow * pow31_seg(seg0);
             const uint32_t q = kLanePow.v[threadIdx.x & 63u] * p0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -385,7 +412,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
                 if ((threadIdx.x & 63u) == 0) a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum;
             }
         } else {
-            const uint32_t p = dpow31(a.hbase + off);
+            const uint32_t p = a.hpow * pow31_seg(static_cast<uint32_t>(off >> 4));
 #pragma unroll
             for (int r = 0; r < R; ++r)
                 atomicAdd(reinterpret_cast<unsigned*>(a.hashes) + static_cast<uint64_t>(stripe) * a.hstride + r,
@@ -562,7 +589,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     a.lstride = static_cast<uint32_t>(p.cols);
     for (int j = 0; j < K; ++j) a.clen[j] = p.clen[j];
     a.hstride = p.hash_stride;
-    a.hbase = p.hash_base;
+    a.hpow = pow31(p.hash_base);
     for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(p.coef[(r0 + r) * p.cols + j]);
     const int block = block_for(p.len, R * K);

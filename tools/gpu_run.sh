@@ -34,6 +34,9 @@ for step in "$@"; do
             -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $?
         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run \
             -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $? ;;
+    profcfg)  # rocprof kernel stats of one bench config: PROF_CFG="--config hashed ..."
+        run profcfg 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profcfg_$TAG -o run \
+            -- python3 bench.py ${PROF_CFG:-} --no-cpu --no-host --steps 20 --warmup 3 || exit $? ;;
     tune) run tune 600 tools/tune/tune_apply || exit $? ;;
     envprobe)  # host facts for DESIGN.md: CPU model, ISA-L presence (for a dlopen cross-check)
         { lscpu | grep -E "Model name|^CPU\(s\)|Flags" | cut -c1-200; echo "nproc=$(nproc)";
