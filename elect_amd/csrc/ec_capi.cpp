@@ -301,11 +301,8 @@ int elect_ec_encode_batch_hashed(const elect_ec_coder* coder, size_t chunk_size,
     if (!valid_coder(coder) || !d_hashes) return ELECT_EC_EINVAL;
     if (num_stripes == 0) return ELECT_EC_OK;
     if (chunk_size > 0 && (!data.base || !parity.base)) return ELECT_EC_EINVAL;
-    hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_hashes),
-                                     static_cast<int>(elect::kern::pow31(chunk_size)),
-                                     num_stripes * static_cast<size_t>(coder->m), as_stream(stream));
-    if (e != hipSuccess || chunk_size == 0) return map_hip(e);
     ApplyParams p;
+    p.hash_seed = true;  // the launcher produces 31^len + sum (no separate memset where it can)
     p.len = chunk_size;
     p.stripes = num_stripes;
     p.cols = coder->k;

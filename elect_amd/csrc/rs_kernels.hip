@@ -254,7 +254,8 @@ struct FastArgs {
     int32_t* hashes;        // optional parity hashes, [stripe][hstride] (row r at +r)
     uint32_t hstride;
     uint32_t hpow;          // 31^(hash offset of byte 0 of this launch window)
-    uint32_t* hpart;        // per-wave partial sums [wave][R] (waves wholly inside one stripe)
+    uint32_t* hpart;        // per-wave partial sums [wave][R]: the wave's first stripe
+    uint32_t* hpart_hi;     // assign mode: [wave][R] sums of a straddling wave's second stripe, else null
     gf::PermTable tab[R][K];
 };
 
@@ -315,8 +316,12 @@ template <int K, int R, bool PAD>
 __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
-    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = idx < a.total;
+    const uint32_t idx_raw = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = idx_raw < a.total;
+    // Lanes past the end of the launch redo the last segment (identical bytes
+    // to identical addresses) rather than leave the wave, so wave-wide hash
+    // reductions see every lane; their hash terms are zeroed.
+    const uint32_t idx = live ? idx_raw : a.total - 1;
     const uint32_t stripe = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
     const uint64_t off = static_cast<uint64_t>(idx - stripe * a.segs) * 16;
 
@@ -327,7 +332,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
     // (Hoisting the plain launches' data loads the same way measured 2 % slower.)
     bool uniform = false;
     uint32_t sl[K];
-    const uint32_t first = __builtin_amdgcn_readfirstlane(idx);
+    const uint32_t first = __builtin_amdgcn_readfirstlane(idx_raw);
     if (PAD && a.lens && first < a.total) {  // (a wholly dead wave reads nothing)
         const uint32_t s0 = static_cast<uint32_t>((static_cast<uint64_t>(first) * a.magic) >> a.shift);
         const uint32_t s1 = static_cast<uint32_t>((static_cast<uint64_t>(first + 63) * a.magic) >> a.shift);
@@ -338,7 +343,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
     }
 
     stage_tables(a, tl);
-    if (!live) return;
+    if (first >= a.total) return;  // wave-uniform: a wholly dead wave
     if (!PAD) {
 #pragma unroll
         for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + stripe * a.ss[j] + off);
@@ -411,7 +416,20 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
                 const uint32_t sum = wave_sum(horner31(acc[r]) * q);
                 if ((threadIdx.x & 63u) == 0) a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum;
             }
-        } else {
+        } else if (a.hpart_hi) {  // assign mode: a wave straddling two stripes (or the launch's end)
+            const uint32_t p = live ? a.hpow * pow31_seg(static_cast<uint32_t>(off >> 4)) : 0u;
+            const bool lo = stripe == s_first;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t v = horner31(acc[r]) * p;
+                const uint32_t sum_lo = wave_sum(lo ? v : 0u);
+                const uint32_t sum_hi = wave_sum(lo ? 0u : v);
+                if ((threadIdx.x & 63u) == 0) {
+                    a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum_lo;
+                    a.hpart_hi[static_cast<uint64_t>(first >> 6) * R + r] = sum_hi;
+                }
+            }
+        } else if (live) {
             const uint32_t p = a.hpow * pow31_seg(static_cast<uint32_t>(off >> 4));
 #pragma unroll
             for (int r = 0; r < R; ++r)
@@ -542,24 +560,34 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
 template <int K>
 constexpr int lens_unroll() { return K <= 4 ? AB_PAD_U4 : 1; }
 
-// Sum the per-wave hash partials of each (stripe, row): the waves lying wholly
-// inside stripe s are [ceil(s*segs/64), floor((s+1)*segs/64)); straddling waves
-// already added theirs atomically.  One wave per (stripe, row): lanes stride
-// over the partials, then a wave sum; lane 0 is the sole writer.
-__global__ __launch_bounds__(kBlock) void hash_reduce(const uint32_t* __restrict__ part, int32_t* hashes,
-                                                      uint32_t hstride, int rows, uint32_t segs, uint32_t stripes)
+// Sum the per-wave hash partials of each (stripe, row); one wave per pair:
+// lanes stride over the partials, then a wave sum; lane 0 is the sole writer.
+// Add mode: the waves lying wholly inside stripe s are
+// [ceil(s*segs/64), floor((s+1)*segs/64)); straddling waves already added
+// theirs atomically; the entry (seeded with 31^len) is incremented.
+// Assign mode (hi != null, segs >= 64): every wave of [floor(s*segs/64),
+// floor(((s+1)*segs-1)/64)] contributes its first-stripe sum if it starts
+// inside s, else its second-stripe sum; the entry becomes seed + sum.
+__global__ __launch_bounds__(kBlock) void hash_reduce(const uint32_t* __restrict__ part, const uint32_t* __restrict__ hi,
+                                                      int32_t* hashes, uint32_t hstride, int rows, uint32_t segs,
+                                                      uint32_t stripes, uint32_t seed)
 {
     const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // (stripe, row) of this wave
     if (t >= stripes * static_cast<uint32_t>(rows)) return;
     const uint32_t s = t / rows, r = t % rows, lane = threadIdx.x & 63u;
-    const uint64_t w0 = (static_cast<uint64_t>(s) * segs + 63) / 64;
-    const uint64_t w1 = (static_cast<uint64_t>(s) + 1) * segs / 64;
+    const uint64_t start = static_cast<uint64_t>(s) * segs;
     uint32_t sum = 0;
-    for (uint64_t w = w0 + lane; w < w1; w += 64) sum += part[w * rows + r];
+    if (hi) {
+        const uint64_t w0 = start / 64, w1 = (start + segs - 1) / 64;
+        for (uint64_t w = w0 + lane; w <= w1; w += 64) sum += (w * 64 >= start ? part : hi)[w * rows + r];
+    } else {
+        const uint64_t w0 = (start + 63) / 64, w1 = (start + segs) / 64;
+        for (uint64_t w = w0 + lane; w < w1; w += 64) sum += part[w * rows + r];
+    }
     sum = wave_sum(sum);
     if (lane == 0) {
         uint32_t* h = reinterpret_cast<uint32_t*>(hashes) + static_cast<uint64_t>(s) * hstride + r;
-        *h += sum;
+        *h = (hi ? seed : *h) + sum;
     }
 }
 
@@ -593,6 +621,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(p.coef[(r0 + r) * p.cols + j]);
     const int block = block_for(p.len, R * K);
+    const bool hash_assign = p.hashes && p.hash_seed;  // launch_apply chose assign mode
     const uint64_t per_launch = kMaxIndex / segs64;  // stripes per launch keeping idx < 2^31
     for (uint64_t s0 = 0; s0 < p.stripes; s0 += per_launch) {
         const uint64_t ns = std::min<uint64_t>(per_launch, p.stripes - s0);
@@ -608,10 +637,13 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         a.hashes = p.hashes ? p.hashes + s0 * p.hash_stride + r0 : nullptr;
         a.total = static_cast<uint32_t>(ns * segs64);
         a.hpart = nullptr;
-        if (a.hashes) {  // stream-ordered scratch for the per-wave partial sums
-            const size_t bytes = (static_cast<size_t>(a.total) / 64 + 1) * R * sizeof(uint32_t);
-            const hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&a.hpart), bytes, stream);
+        a.hpart_hi = nullptr;
+        if (a.hashes) {  // stream-ordered scratch for the per-wave partial sums (lo, then hi)
+            const size_t n = (static_cast<size_t>(a.total) / 64 + 1) * R;
+            const hipError_t e =
+                hipMallocAsync(reinterpret_cast<void**>(&a.hpart), (hash_assign ? 2 : 1) * n * sizeof(uint32_t), stream);
             if (e != hipSuccess) return e;
+            if (hash_assign) a.hpart_hi = a.hpart + n;
         }
         bool lens_path = false;
         if constexpr (PAD) {
@@ -631,7 +663,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         if (e == hipSuccess && a.hashes) {
             const uint32_t n = static_cast<uint32_t>(ns) * R;  // one wave each
             hipLaunchKernelGGL(hash_reduce, dim3((n + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, stream, a.hpart,
-                               a.hashes, a.hstride, R, a.segs, static_cast<uint32_t>(ns));
+                               a.hpart_hi, a.hashes, a.hstride, R, a.segs, static_cast<uint32_t>(ns), pow31(p.len));
             e = hipGetLastError();
         }
         if (a.hpart) {
@@ -901,10 +933,24 @@ bool apply_is_aligned(const ApplyParams& p)
     return true;
 }
 
-hipError_t launch_apply(const ApplyParams& p, hipStream_t stream)
+hipError_t launch_apply(const ApplyParams& p_in, hipStream_t stream)
 {
-    if (p.cols < 1 || p.cols > kMaxCols || p.rows < 1 || p.rows > kMaxRows) return hipErrorInvalidValue;
-    if (p.len == 0 || p.stripes == 0) return hipSuccess;
+    if (p_in.cols < 1 || p_in.cols > kMaxCols || p_in.rows < 1 || p_in.rows > kMaxRows) return hipErrorInvalidValue;
+    if (p_in.stripes == 0) return hipSuccess;
+    ApplyParams p = p_in;
+    if (p.hashes && p.hash_seed) {
+        // Assign mode needs the fast kernel with >= 64 segments per stripe (every
+        // wave within two stripes); anything else seeds the entries and adds.
+        const bool fast = apply_is_aligned(p) && (!p.padded || p.cols <= kMaxPadCols);
+        const uint64_t segs = p.padded ? (p.len + 15) / 16 : p.len / 16;
+        if (!fast || segs < 64) {
+            const hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.hashes),
+                                                   static_cast<int>(pow31(p.len)), p.stripes * p.hash_stride, stream);
+            if (e != hipSuccess) return e;
+            p.hash_seed = false;
+        }
+    }
+    if (p.len == 0) return hipSuccess;
     if (p.padded) {
         for (int j = 0; j < p.cols; ++j)
             if (!p.lens && p.clen[j] > p.len) return hipErrorInvalidValue;

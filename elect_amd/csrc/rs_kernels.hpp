@@ -54,6 +54,12 @@ struct ApplyParams {
     int32_t* hashes = nullptr;
     uint32_t hash_stride = 0;
     uint64_t hash_base = 0;
+    // hash_seed: the entries are NOT initialised; launch_apply produces
+    // 31^len + sum itself.  Where every wave of the fast kernel covers at most
+    // two stripes (>= 64 segments per stripe) the per-wave partials are summed
+    // and assigned by hash_reduce with no memset and no atomics; otherwise the
+    // launcher seeds the entries (hipMemsetD32Async) and the kernels add.
+    bool hash_seed = false;
 };
 
 // 31^e mod 2^32 (host side of the parity hash).

@@ -361,11 +361,12 @@ def test_host_path_concurrent_callers(dev, oracle):
 
 
 @pytest.mark.parametrize("k,m,L", [(4, 2, 65536), (4, 2, 4099), (4, 2, 1), (4, 2, 15), (8, 4, 1024), (4, 2, 1 << 20),
-                                   (4, 10, 333), (3, 2, 4404020 // 64)])
+                                   (4, 10, 333), (3, 2, 4404020 // 64), (4, 2, 1040), (6, 3, 16008)])
 def test_encode_batch_hashed_matches_java_hashcode(dev, oracle, k, m, L):
     """Fused parity hash == java.nio.ByteBuffer.hashCode() of each parity unit
-    (ECMessageVerbHandler.java:326-329), incl. tails, waves straddling stripes,
-    and row groups (m > 4)."""
+    (ECMessageVerbHandler.java:326-329), incl. tails, waves straddling stripes
+    (1040, 16008: every / some waves; the launch's last wave partial), the
+    memset-and-add mode (< 64 segments per stripe) and row groups (m > 4)."""
     from elect_amd.batch import encode_batch_hashed
     from elect_amd.coder import RSCoder, java_bytebuffer_hash
     rng = np.random.default_rng(L + 13 * k)
