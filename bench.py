@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--m", type=int, default=2)
     ap.add_argument("--chunk", type=int, default=65536)
     ap.add_argument("--stripes", type=int, default=4096)
+    ap.add_argument("--unit-gap", type=int, default=0,
+                    help="headline layout experiment: bytes of gap after each unit in HBM ([B][k+m][L+gap])")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU-baseline work time (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -426,7 +428,7 @@ def config_padded(args, world, rank, dev):
             "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "gf_apply_x16<4,2,padded>", "algorithmic_bytes_per_launch": alg,
+                         "kernel": "gf_apply_lens<4,2,4> (padded, per-stripe lengths)", "algorithmic_bytes_per_launch": alg,
                          "fill": round(valid / (B * k * L), 3)},
             "config": {"workload": f"{B} stripes, content lengths " + (f"uniform in [0, {L}]" if args.pad_fill == "random"
                                                                      else f"{args.pad_fill} x {L}"),
@@ -497,9 +499,9 @@ def main():
     n = k + m
     coder = RSCoder(k, m)
     g = torch.Generator(device=dev).manual_seed(0xE1EC7 + rank)
-    stripe = torch.empty((B, n, L), dtype=torch.uint8, device=dev)
+    stripe = torch.empty((B, n, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L]
     stripe[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g)
-    rebuilt = torch.empty((B, 1, L), dtype=torch.uint8, device=dev)
+    rebuilt = torch.empty((B, 1, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L]
     survivors = list(range(1, k + 1))
     stream = torch.cuda.current_stream()
 

@@ -37,6 +37,11 @@ for step in "$@"; do
     profcfg)  # rocprof kernel stats of one bench config: PROF_CFG="--config hashed ..."
         run profcfg 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profcfg_$TAG -o run \
             -- python3 bench.py ${PROF_CFG:-} --no-cpu --no-host --steps 20 --warmup 3 || exit $? ;;
+    sweep)  # bench argument sweep, interleaved 3x: SWEEP_ARGS="--unit-gap 0;--unit-gap 256"
+        IFS=';' read -ra SW <<< "${SWEEP_ARGS:-}"
+        for i in 1 2 3; do for n in "${!SW[@]}"; do
+            run "ab_s${n}_headline_$i" 300 python bench.py ${SW[$n]} --no-cpu --no-host --steps 50 || exit $?
+        done; done ;;
     tune) run tune 600 tools/tune/tune_apply || exit $? ;;
     envprobe)  # host facts for DESIGN.md: CPU model, ISA-L presence (for a dlopen cross-check)
         { lscpu | grep -E "Model name|^CPU\(s\)|Flags" | cut -c1-200; echo "nproc=$(nproc)";
