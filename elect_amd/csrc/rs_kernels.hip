@@ -312,7 +312,10 @@ __device__ __forceinline__ void stage_tables(const FastArgs<K, R>& a, uint32_t* 
     __syncthreads();
 }
 
-template <int K, int R, bool PAD>
+// HASH instances (encode shapes only) carry the parity-hash epilogue; keeping
+// it out of the others saved RS(12,8) encode ~120 v_mov (acc kept live across
+// the stores) and 4 VGPRs.
+template <int K, int R, bool PAD, bool HASH>
 __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
@@ -321,7 +324,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
     // Lanes past the end of the launch redo the last segment (identical bytes
     // to identical addresses) rather than leave the wave, so wave-wide hash
     // reductions see every lane; their hash terms are zeroed.
-    const uint32_t idx = live ? idx_raw : a.total - 1;
+    const uint32_t idx = (!HASH || live) ? idx_raw : a.total - 1;
     const uint32_t stripe = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
     const uint64_t off = static_cast<uint64_t>(idx - stripe * a.segs) * 16;
 
@@ -343,7 +346,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
     }
 
     stage_tables(a, tl);
-    if (first >= a.total) return;  // wave-uniform: a wholly dead wave
+    if (HASH ? first >= a.total : !live) return;  // HASH: only wholly dead waves leave
     if (!PAD) {
 #pragma unroll
         for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + stripe * a.ss[j] + off);
@@ -390,7 +393,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         for (int r = 0; r < R; ++r) store_partial(a.dp[r] + stripe * a.ds[r] + off, acc[r], n);
     }
 
-    if (a.hashes) {  // fused parity hash: one integer atomic per wave and row
+    if (HASH && a.hashes) {  // fused parity hash
         if (PAD && off + 16 > a.len) {  // a partial last segment: zero the bytes past len
             const uint32_t n = static_cast<uint32_t>(a.len - off);
 #pragma unroll
@@ -598,8 +601,16 @@ __global__ __launch_bounds__(kBlock) void hash_reduce(const uint32_t* __restrict
 #ifdef AB_BLOCK  // A/B builds (tools/ab_build.sh): one block size for every launch
 inline int block_for(uint64_t, int) { return AB_BLOCK; }
 #else
+#ifdef AB_BLOCK  // A/B builds (tools/ab_build.sh): one block size for every launch
+inline int block_for(uint64_t, int) { return AB_BLOCK; }
+#elif defined(AB_BLOCK_COEFS)  // A/B: 128 threads from this many coefficients
+inline int block_for(uint64_t len, int coefs) { return (len <= 4096 || coefs >= AB_BLOCK_COEFS) ? 128 : kBlock; }
+#else
 inline int block_for(uint64_t len, int coefs) { return (len <= 4096 || coefs >= 16) ? 128 : kBlock; }
 #endif
+#endif
+
+constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches are encodes
 
 template <int K, int R, bool PAD>
 hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
@@ -657,7 +668,11 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         }
         if (!lens_path) {
             const uint32_t grid = (a.total + block - 1) / block;
-            hipLaunchKernelGGL((gf_apply_x16<K, R, PAD>), dim3(grid), dim3(block), 0, stream, a);
+            if (!a.hashes) {
+                hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, false>), dim3(grid), dim3(block), 0, stream, a);
+            } else if constexpr (K <= kMaxHashCols) {
+                hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, true>), dim3(grid), dim3(block), 0, stream, a);
+            }  // (launch_apply rejects hashed launches wider than kMaxHashCols)
         }
         hipError_t e = hipGetLastError();
         if (e == hipSuccess && a.hashes) {
@@ -938,6 +953,7 @@ hipError_t launch_apply(const ApplyParams& p_in, hipStream_t stream)
     if (p_in.cols < 1 || p_in.cols > kMaxCols || p_in.rows < 1 || p_in.rows > kMaxRows) return hipErrorInvalidValue;
     if (p_in.stripes == 0) return hipSuccess;
     ApplyParams p = p_in;
+    if (p.hashes && p.cols > kMaxHashCols) return hipErrorInvalidValue;  // hashes are an encode feature
     if (p.hashes && p.hash_seed) {
         // Assign mode needs the fast kernel with >= 64 segments per stripe (every
         // wave within two stripes); anything else seeds the entries and adds.

@@ -97,7 +97,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 __device__ uint32_t* g_hash;  // set by the host before hash variants run
 enum Load { kPlain = 0, kNTL = 1, kNTS = 2, kNT = 3 };
 
-template <int K, int R, int U, int BLOCK, int MODE, int LD, bool GRIDSTRIDE, int ORDER = 0>
+template <int K, int R, int U, int BLOCK, int MODE, int LD, bool GRIDSTRIDE, int ORDER = 0, bool ADJ = false>
 __global__ __launch_bounds__(BLOCK) void kern(const Args<K, R> a)
 {
     // ORDER 2: column-outer with the byte-shuffle tables staged in LDS
@@ -120,7 +120,9 @@ __global__ __launch_bounds__(BLOCK) void kern(const Args<K, R> a)
         bool live[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t idx = first + u * BLOCK;
+            // ADJ: a wave's U loads per column cover U KiB back to back; else BLOCK*16 B apart
+            const uint32_t idx = ADJ ? blockIdx.x * (BLOCK * U) + (threadIdx.x >> 6) * (64 * U) + u * 64 + (threadIdx.x & 63)
+                                     : first + u * BLOCK;
             const uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
             stripe[u] = s;
             off[u] = static_cast<uint64_t>(idx - s * a.segs) * 16;
@@ -310,7 +312,7 @@ struct Runner {
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_hash), &hbuf, sizeof(hbuf)));
     }
 
-    template <int U, int BLOCK, int MODE, int LD, bool GS, int ORDER = 0>
+    template <int U, int BLOCK, int MODE, int LD, bool GS, int ORDER = 0, bool ADJ = false>
     float time_one(int occ_blocks_per_cu, int iters)
     {
         const uint32_t per_block = BLOCK * U;
@@ -322,7 +324,7 @@ struct Runner {
         std::vector<float> ts;
         for (int i = 0; i < iters; ++i) {
             CK(hipEventRecord(e0));
-            hipLaunchKernelGGL((kern<K, R, U, BLOCK, MODE, LD, GS, ORDER>), dim3(grid), dim3(BLOCK), 0, 0, a);
+            hipLaunchKernelGGL((kern<K, R, U, BLOCK, MODE, LD, GS, ORDER, ADJ>), dim3(grid), dim3(BLOCK), 0, 0, a);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms = 0;
@@ -383,23 +385,13 @@ static void sweep(const Shape& s)
     auto rec = [&](const char* n, float ms, bool check) { rows.push_back({n, ms, check ? rn.same() : true, check}); };
     for (int round = 0; round < 3; ++round) {
         rows.clear();
-        rec("U1 ntboth roworder", rn.template time_one<1, 256, kGF, kNT, false, 0>(0, it), true);
-        rec("U1 ntload roworder", rn.template time_one<1, 256, kGF, kNTL, false, 0>(0, it), true);
-        rec("U1 plain roworder", rn.template time_one<1, 256, kGF, kPlain, false, 0>(0, it), true);
-        rec("U1 ntboth colorder", rn.template time_one<1, 256, kGF, kNT, false, 1>(0, it), true);
-        rec("U1 ntload colorder", rn.template time_one<1, 256, kGF, kNTL, false, 1>(0, it), true);
-        rec("U1 ntboth LDS-tab", rn.template time_one<1, 256, kGF, kNT, false, 2>(0, it), true);
-        rec("U1 ntload LDS-tab", rn.template time_one<1, 256, kGF, kNTL, false, 2>(0, it), true);
-        rec("U1 plain LDS-tab", rn.template time_one<1, 256, kGF, kPlain, false, 2>(0, it), true);
-        rec("U1 ntstore LDS-tab", rn.template time_one<1, 256, kGF, kNTS, false, 2>(0, it), true);
-        rec("U1 b128 ntboth LDS-tab", rn.template time_one<1, 128, kGF, kNT, false, 2>(0, it), true);
-        rec("U1 b128 ntboth colorder", rn.template time_one<1, 128, kGF, kNT, false, 1>(0, it), true);
-        rec("U1 b128 ntload colorder", rn.template time_one<1, 128, kGF, kNTL, false, 1>(0, it), true);
-        rec("U1 nt LDS hash-atomic", rn.template time_one<1, 256, kHashAtomic, kNT, false, 2>(0, it), true);
-        rec("U1 nt LDS hash-scratch", rn.template time_one<1, 256, kHashScratch, kNT, false, 2>(0, it), true);
-        rec("U1 nt LDS hash-compute", rn.template time_one<1, 256, kHashLocal, kNT, false, 2>(0, it), true);
-        rec("U1 XOR-only ntload", rn.template time_one<1, 256, kXor, kNTL, false>(0, it), false);
+        rec("U1 b256 nt LDS-tab (product)", rn.template time_one<1, 256, kGF, kNT, false, 2>(0, it), true);
+        rec("U2 b256 nt LDS-tab adjacent", rn.template time_one<2, 256, kGF, kNT, false, 2, true>(0, it), true);
+        rec("U4 b256 nt LDS-tab adjacent", rn.template time_one<4, 256, kGF, kNT, false, 2, true>(0, it), true);
+        rec("U2 b128 nt LDS-tab adjacent", rn.template time_one<2, 128, kGF, kNT, false, 2, true>(0, it), true);
+        rec("U2 b256 nt LDS-tab 4KiB apart", rn.template time_one<2, 256, kGF, kNT, false, 2>(0, it), true);
         rec("U1 XOR-only nt both", rn.template time_one<1, 256, kXor, kNT, false>(0, it), false);
+        rec("U2 XOR-only nt both adjacent", rn.template time_one<2, 256, kXor, kNT, false, 0, true>(0, it), false);
         // restore reference output for later variants' checks
         rn.template time_one<2, 256, kGF, kPlain, false>(0, 1);
     }
