@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--m", type=int, default=2)
     ap.add_argument("--chunk", type=int, default=65536)
     ap.add_argument("--stripes", type=int, default=4096)
+    ap.add_argument("--layout", choices=("stripe", "unit"), default="stripe",
+                    help="HBM layout of the stripes ([B][k+m][L] or [k+m][B][L]); headline and mixed")
     ap.add_argument("--unit-gap", type=int, default=0,
                     help="headline layout experiment: bytes of gap after each unit in HBM ([B][k+m][L+gap])")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -233,7 +235,10 @@ def config_mixed(args, world, rank, dev):
     for L in (1024, 4096, 1 << 20):
         total = (1 << 30) // (k * L)
         b, e = partition_by_bytes([k * L] * total, world, rank)
-        st = torch.empty((e - b, k + m, L), dtype=torch.uint8, device=dev)
+        if args.layout == "unit":  # [k+m][B][L]: every unit column is one contiguous region
+            st = torch.empty((k + m, e - b, L), dtype=torch.uint8, device=dev).transpose(0, 1)
+        else:                      # [B][k+m][L]: stripes back to back
+            st = torch.empty((e - b, k + m, L), dtype=torch.uint8, device=dev)
         st[:, :k] = torch.randint(0, 256, (e - b, k, L), dtype=torch.uint8, device=dev)
         classes.append((L, st, torch.empty((e - b, 1, L), dtype=torch.uint8, device=dev)))
 
@@ -245,12 +250,30 @@ def config_mixed(args, world, rank, dev):
     dt = timed(step, args.steps, args.warmup, world)
     ok = all(torch.equal(out[:, 0], st[:, 0]) for _, st, out in classes)
     data = 2 * 3 * (1 << 30)  # enc + dec, 3 classes, all ranks together
+    per_class = {}  # outside the timed region: each class's kernels by HIP events (median of 9)
+    for L, st, out in classes:
+        t = {"encode": [], "decode": []}
+        for _ in range(9):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ev[0].record()
+            encode_batch(coder, st[:, :k], st[:, k:])
+            ev[1].record()
+            decode_batch(coder, st, [1, 2, 3, 4], [0], out, inputs_by_unit=True)
+            ev[2].record()
+            torch.cuda.synchronize()
+            t["encode"].append(ev[0].elapsed_time(ev[1]))
+            t["decode"].append(ev[1].elapsed_time(ev[2]))
+        B = st.shape[0]
+        enc_ms, dec_ms = sorted(t["encode"])[4], sorted(t["decode"])[4]
+        per_class[f"{L}B"] = {"encode_frac": round(B * (k + m) * L / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "decode_frac": round(B * (k + 1) * L / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     return {"metric": "GiB/s device-resident RS(6,4) encode+decode, mixed 1 KiB/4 KiB/1 MiB chunks",
             "value": round(args.steps * data / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic", "verified": ok,
-            "config": {"workload": "RS(6,4) encode+decode (erase 0), 1 GiB data per class "
+            "data": "synthetic", "verified": ok, "classes": per_class,
+            "config": {"layout": "[k+m][B][L] unit-major" if args.layout == "unit" else "[B][k+m][L] stripe-major",
+                       "workload": "RS(6,4) encode+decode (erase 0), 1 GiB data per class "
                                    "(1 KiB x 262144, 4 KiB x 65536, 1 MiB x 256 stripes) over all ranks",
                        "parallelism": f"per-class byte-balanced stripe partition x{world}"}}
 
@@ -516,7 +539,10 @@ def main():
     n = k + m
     coder = RSCoder(k, m)
     g = torch.Generator(device=dev).manual_seed(0xE1EC7 + rank)
-    stripe = torch.empty((B, n, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L]
+    if args.layout == "unit":  # [k+m][B][L] layout experiment
+        stripe = torch.empty((n, B, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L].transpose(0, 1)
+    else:
+        stripe = torch.empty((B, n, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L]
     stripe[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g)
     rebuilt = torch.empty((B, 1, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L]
     survivors = list(range(1, k + 1))

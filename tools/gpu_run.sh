@@ -40,7 +40,7 @@ for step in "$@"; do
     sweep)  # bench argument sweep, interleaved 3x: SWEEP_ARGS="--unit-gap 0;--unit-gap 256"
         IFS=';' read -ra SW <<< "${SWEEP_ARGS:-}"
         for i in 1 2 3; do for n in "${!SW[@]}"; do
-            run "ab_s${n}_headline_$i" 300 python bench.py ${SW[$n]} --no-cpu --no-host --steps 50 || exit $?
+            run "ab_s${n}_${SWEEP_CFG:-headline}_$i" 300 python bench.py --config ${SWEEP_CFG:-headline} ${SW[$n]} --no-cpu --no-host --steps ${SWEEP_STEPS:-50} || exit $?
         done; done ;;
     tune) run tune 600 tools/tune/tune_apply || exit $? ;;
     envprobe)  # host facts for DESIGN.md: CPU model, ISA-L presence (for a dlopen cross-check)
