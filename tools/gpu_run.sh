@@ -61,6 +61,11 @@ for step in "$@"; do
         run bench_hashed 400 python bench.py --config hashed || exit $?
         run bench_hashed_1M 400 python bench.py --config hashed --chunk 1048576 || exit $? ;;
     hostsweep) run hostsweep 600 python tools/tune/host_sweep.py || exit $? ;;
+    copysizes) run copysizes 600 python tools/tune/host_sweep.py copysizes || exit $? ;;
+    staged)
+        for node in 0 1; do
+            HOST_NUMA=$node run staged_numa$node 600 python tools/tune/host_sweep.py staged || exit $?
+        done ;;
     batching)
         for L in 4404020 65536; do for T in 16 64; do for B in "" "--batch"; do
             run "bench_hostpath_L${L}_T${T}${B}" 300 python bench.py --config hostpath --threads $T --host-chunk $L $B || exit $?

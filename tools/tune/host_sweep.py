@@ -15,6 +15,20 @@ from elect_amd.batch import encode_batch  # noqa: E402
 from elect_amd.coder import RSCoder  # noqa: E402
 
 GIB = float(1 << 30)
+
+
+def _cpulist(spec):
+    cpus = set()
+    for part in spec.strip().split(","):
+        a, _, b = part.partition("-")
+        cpus.update(range(int(a), int(b or a) + 1))
+    return cpus
+
+
+if os.environ.get("HOST_NUMA"):  # run (and first-touch pinned memory) on one NUMA node's CPUs
+    node = os.environ["HOST_NUMA"]
+    os.sched_setaffinity(0, _cpulist(open(f"/sys/devices/system/node/node{node}/cpulist").read()))
+    print(f"affinity: NUMA node {node}", flush=True)
 dev = torch.device("cuda:0")
 k, m, L = 4, 2, 65536
 coder = RSCoder(k, m)
@@ -73,6 +87,53 @@ def pinned_pipeline(nstreams, chunk, total_stripes=2048):
     return 2 * total_stripes * k * L / dt / GIB
 
 
+def staged_pipeline(chunk, ring, total_stripes=4096):
+    """Three streams (H2D, compute, D2H) over a ring of device buffers, chained
+    by events: the copy engines of both directions stay busy continuously."""
+    nch = total_stripes // chunk
+    h_data = torch.randint(0, 256, (total_stripes, k, L), dtype=torch.uint8).pin_memory()
+    h_par = torch.empty((total_stripes, m, L), dtype=torch.uint8).pin_memory()
+    s_in, s_cmp, s_out = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    dd = [torch.empty((chunk, k, L), dtype=torch.uint8, device=dev) for _ in range(ring)]
+    dp = [torch.empty((chunk, m, L), dtype=torch.uint8, device=dev) for _ in range(ring)]
+
+    def run():
+        ev_in = [None] * nch
+        ev_cmp = [None] * nch
+        ev_out = [None] * nch
+        for c in range(nch):
+            r = c % ring
+            with torch.cuda.stream(s_in):
+                if c >= ring:
+                    s_in.wait_event(ev_cmp[c - ring])  # buffer r's data consumed
+                dd[r].copy_(h_data[c * chunk:(c + 1) * chunk], non_blocking=True)
+                ev_in[c] = torch.cuda.Event()
+                ev_in[c].record(s_in)
+            with torch.cuda.stream(s_cmp):
+                s_cmp.wait_event(ev_in[c])
+                if c >= ring:
+                    s_cmp.wait_event(ev_out[c - ring])  # buffer r's parity drained
+                encode_batch(coder, dd[r], dp[r], stream=s_cmp)
+                ev_cmp[c] = torch.cuda.Event()
+                ev_cmp[c].record(s_cmp)
+            with torch.cuda.stream(s_out):
+                s_out.wait_event(ev_cmp[c])
+                h_par[c * chunk:(c + 1) * chunk].copy_(dp[r], non_blocking=True)
+                ev_out[c] = torch.cuda.Event()
+                ev_out[c].record(s_out)
+        torch.cuda.synchronize()
+
+    run()
+    t0 = time.perf_counter()
+    run()
+    run()
+    dt = time.perf_counter() - t0
+    ref = torch.empty((chunk, m, L), dtype=torch.uint8, device=dev)
+    encode_batch(coder, h_data[-chunk:].to(dev), ref)
+    assert torch.equal(ref.cpu(), h_par[-chunk:]), "staged pipeline parity mismatch"
+    return 2 * total_stripes * k * L / dt / GIB
+
+
 def pageable(threads, Lc=4404020, calls=8):
     bufs = []
     for t in range(threads):
@@ -97,6 +158,40 @@ def pageable(threads, Lc=4404020, calls=8):
 
 
 if __name__ == "__main__":
+    if "copysizes" in sys.argv:  # raw pinned copy rate by transfer size, each direction alone and both
+        big = 1 << 30
+        h = torch.empty(big, dtype=torch.uint8).pin_memory()
+        h2 = torch.empty(big, dtype=torch.uint8).pin_memory()
+        d = torch.empty(big, dtype=torch.uint8, device=dev)
+        d2 = torch.empty(big, dtype=torch.uint8, device=dev)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        for mib in (1, 2, 4, 8, 12, 16, 24, 32, 48, 64):
+            n = mib << 20
+            cnt = big // n
+            res = []
+            for mode in ("H2D", "D2H", "both"):
+                for warm in (0, 1):
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    for i in range(cnt):
+                        if mode in ("H2D", "both"):
+                            with torch.cuda.stream(s1):
+                                d[i * n:(i + 1) * n].copy_(h[i * n:(i + 1) * n], non_blocking=True)
+                        if mode in ("D2H", "both"):
+                            with torch.cuda.stream(s2):
+                                h2[i * n:(i + 1) * n].copy_(d2[i * n:(i + 1) * n], non_blocking=True)
+                    torch.cuda.synchronize()
+                    dt = time.perf_counter() - t0
+                res.append(f"{mode} {(2 if mode == 'both' else 1) * big / dt / 1e9:.1f}")
+            print(f"copy {mib:3d} MiB: " + "  ".join(res) + " GB/s", flush=True)
+        sys.exit(0)
+    if "staged" in sys.argv:
+        pcie()
+        for ch in (16, 64, 128):
+            for ring in (3,):
+                print(f"staged pipeline chunk={ch} stripes ({ch * k * L >> 20} MiB data) ring={ring}: "
+                      f"{staged_pipeline(ch, ring):.2f} GiB/s data", flush=True)
+        sys.exit(0)
     pcie()
     for ns in (1, 2, 3, 4):
         for ch in (32, 128, 512):
