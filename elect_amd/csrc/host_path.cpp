@@ -329,22 +329,21 @@ public:
                     }
             }
             if (slab) break;
-            cv_.notify_all();
-            cv_.wait(lock);
+            cv_worker_.notify_one();  // the open batch was closed: let it leave
+            cv_slot_.wait(lock);      // until an arena is free again
         }
         const int slot = slab->reserved++;
         slab->readers++;
         if (slab->reserved == slab->capacity) slab->full = true;
-        cv_.notify_all();
+        if (slot == 0 || slab->full) cv_worker_.notify_one();
         lock.unlock();
 
         const size_t in_stride = static_cast<size_t>(slab->cols) * pitch;
         for (int j = 0; j < op.cols; ++j) std::memcpy(slab->pin_in + slot * in_stride + j * pitch, op.in[j], len);
 
         lock.lock();
-        slab->filled++;
-        cv_.notify_all();
-        cv_.wait(lock, [&] { return slab->state == Slab::kDone; });
+        if (++slab->filled == slab->reserved) cv_worker_.notify_one();
+        slab->done.wait(lock, [&] { return slab->state == Slab::kDone; });
         const int status = slab->status;
         lock.unlock();
 
@@ -356,7 +355,7 @@ public:
         lock.lock();
         if (--slab->readers == 0) {
             slab->state = Slab::kFree;
-            cv_.notify_all();
+            cv_slot_.notify_all();
         }
         return status;
     }
@@ -373,6 +372,7 @@ private:
         uint64_t seq = 0;
         std::chrono::steady_clock::time_point opened;
         uint8_t *pin_in = nullptr, *pin_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+        std::condition_variable done;  // this batch's callers wait here for kDone
         hipStream_t stream = nullptr;
         hipEvent_t h2d_done = nullptr;
 
@@ -426,7 +426,7 @@ private:
         std::unique_lock<std::mutex> lock(mu_);
         for (;;) {
             Slab* s = nullptr;
-            cv_.wait(lock, [&] {
+            cv_worker_.wait(lock, [&] {
                 s = nullptr;
                 for (Slab& x : slabs_)
                     if (x.state == Slab::kOpen && (!s || x.seq < s->seq)) s = &x;
@@ -439,11 +439,11 @@ private:
                 lock.lock();
             } else {
                 const unsigned w = batch_config().window_us.load();
-                if (w) cv_.wait_until(lock, s->opened + std::chrono::microseconds(w), [&] { return s->full; });
+                if (w) cv_worker_.wait_until(lock, s->opened + std::chrono::microseconds(w), [&] { return s->full; });
             }
             s->full = true;
             s->state = Slab::kInFlight;  // no more reservations
-            cv_.wait(lock, [&] { return s->filled == s->reserved; });
+            cv_worker_.wait(lock, [&] { return s->filled == s->reserved; });
             const int n = s->reserved;
             lock.unlock();
             const hipError_t e = issue(*s, n);
@@ -486,13 +486,22 @@ private:
     void finish(Slab* s, int status)  // mu_ held
     {
         s->status = status;
-        s->state = s->readers == 0 ? Slab::kFree : Slab::kDone;
-        cv_.notify_all();
+        if (s->readers == 0) {
+            s->state = Slab::kFree;
+            cv_slot_.notify_all();
+        } else {
+            s->state = Slab::kDone;
+            s->done.notify_all();
+        }
     }
 
     int dev_;
+    // One mutex; three kinds of waiter, so that a state change wakes only the
+    // threads it concerns (one condition variable for all woke every caller on
+    // every reservation: O(callers^2) wake-ups per batch at 64 callers).
     std::mutex mu_;
-    std::condition_variable cv_;
+    std::condition_variable cv_worker_;  // the dispatcher
+    std::condition_variable cv_slot_;    // callers waiting for an arena to reserve in
     bool started_ = false;
     size_t arena_ = 0;
     uint64_t opened_ = 0;
