@@ -58,7 +58,8 @@ def parse():
                          "(RS(12,8) two-erasure decode, 256 KiB, 512 stripes per GPU); hostpath = the "
                          "JNI-style synchronous host-memory encode at ELECT's codeLength")
     ap.add_argument("--threads", type=int, default=16, help="hostpath: concurrent callers")
-    ap.add_argument("--batch", action="store_true", help="hostpath: cross-thread batching on")
+    ap.add_argument("--batch", type=int, default=1, choices=(0, 1),
+                    help="hostpath: cross-thread batching (the library default, 1) or per-thread staging (0)")
     ap.add_argument("--pad-fill", default="random",
                     help="padded: content lengths 'random' (uniform [0, L]) or a fixed fraction of L")
     ap.add_argument("--host-chunk", type=int, default=4404020, help="hostpath: bytes per unit per call")

@@ -290,7 +290,7 @@ BatchConfig& batch_config()
         if (w) c.window_us = static_cast<unsigned>(std::atoi(w));
         if (a && std::atoi(a) > 0) c.arena_bytes = static_cast<size_t>(std::atoi(a)) << 20;
         int expect = -1;
-        c.enabled.compare_exchange_strong(expect, (e && std::atoi(e) > 0) ? 1 : 0);
+        c.enabled.compare_exchange_strong(expect, (!e || std::atoi(e) > 0) ? 1 : 0);  // on unless ELECT_EC_BATCH=0
     }
     return c;
 }

@@ -84,8 +84,8 @@ int elect_ec_device_count(int* count);
  * n = 0 restores the default.  Returns ELECT_EC_EINVAL for an unknown device. */
 int elect_ec_set_host_devices(const int* devices, int n);
 
-/* Cross-thread batching of host-memory calls (off by default; or
- * ELECT_EC_BATCH=1, ELECT_EC_BATCH_WINDOW_US, ELECT_EC_BATCH_ARENA_MB).  While
+/* Cross-thread batching of host-memory calls (on by default; ELECT_EC_BATCH=0
+ * turns it off; ELECT_EC_BATCH_WINDOW_US, ELECT_EC_BATCH_ARENA_MB).  While
  * on, concurrent elect_ec_encode / elect_ec_decode calls of the same shape share
  * one pinned arena, one H2D, one kernel launch and one D2H; each call still
  * returns only when its own outputs are written.  Dispatch is self-clocking: a
@@ -93,7 +93,9 @@ int elect_ec_set_host_devices(const int* devices, int n);
  * an idle device, or after window_us if non-zero), so transfers pipeline.
  * arena_bytes (per direction, x2 arenas, per device) takes effect for devices
  * whose batcher has not started yet.  ELECT issues up to concurrent_ec (64)
- * such calls at once (conf/elect.yaml:598). */
+ * such calls at once (conf/elect.yaml:598): there batching measured 3x the
+ * per-thread path (40.7 vs 12.5 GiB/s on 4.4 MB stripes); a lone caller loses
+ * ~10 % (12.5 vs 13.7 GiB/s), as its stripe is not split into overlapped chunks. */
 int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes);
 
 /* ---- coder lifecycle ----

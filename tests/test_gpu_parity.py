@@ -493,7 +493,7 @@ def test_mixed_size_batch_properties(dev, oracle):
 
 
 def test_cross_thread_batching(dev, oracle):
-    """elect_ec_set_batching: concurrent one-stripe host calls share one arena,
+    """Cross-thread batching (on by default): concurrent one-stripe host calls share one arena,
     H2D, launch and D2H.  Mixed shapes (two lengths, encode and decode) force
     batches to close early and the two arenas to alternate; every call must
     still get exactly its own parity / rebuilt unit."""
@@ -530,13 +530,14 @@ def test_cross_thread_batching(dev, oracle):
             x.start()
         for x in th:
             x.join()
-        # a stripe larger than the arena falls back to the direct path
-        L = 3 << 20
+        # a stripe larger than the arena falls back to the direct path (batching is
+        # on by default, so the batcher may already run with the default 256 MiB arena)
+        L = max(3 << 20, (256 << 20) // k + 4096)
         d = [np.full(L, j + 1, np.uint8) for j in range(k)]
         p = [np.empty(L, np.uint8) for _ in range(m)]
         coder.encode_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L)
         want = enc.encode(d)
         assert all(np.array_equal(a, b) for a, b in zip(p, want))
     finally:
-        _lib.set_batching(False)
+        _lib.set_batching(True)  # the library default
     assert not errors, errors[:5]

@@ -67,8 +67,8 @@ for step in "$@"; do
             HOST_NUMA=$node run staged_numa$node 600 python tools/tune/host_sweep.py staged || exit $?
         done ;;
     batching)
-        for L in 4404020 65536; do for T in ${BATCH_THREADS:-16 64}; do for B in "" "--batch"; do
-            run "bench_hostpath_L${L}_T${T}${B}" 300 python bench.py --config hostpath --threads $T --host-chunk $L $B || exit $?
+        for L in 4404020 65536; do for T in ${BATCH_THREADS:-16 64}; do for B in 0 1; do
+            run "bench_hostpath_L${L}_T${T}_batch$B" 300 python bench.py --config hostpath --threads $T --host-chunk $L --batch $B || exit $?
         done; done; done ;;
     configs)
         run bench_mixed 400 python bench.py --config mixed || exit $?
