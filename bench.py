@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--stripes", type=int, default=4096)
     ap.add_argument("--layout", choices=("stripe", "unit"), default="stripe",
                     help="HBM layout of the stripes ([B][k+m][L] or [k+m][B][L]); headline and mixed")
+    ap.add_argument("--decode-out", choices=("separate", "inplace"), default="separate",
+                    help="headline decode target: a separate [B][1][L] buffer, or the erased unit's own slot")
+    ap.add_argument("--rebuilt-rows", type=int, default=1,
+                    help="layout experiment: the separate decode buffer is [B][rows][L], row 0 used")
     ap.add_argument("--unit-gap", type=int, default=0,
                     help="headline layout experiment: bytes of gap after each unit in HBM ([B][k+m][L+gap])")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -568,9 +572,10 @@ def main():
     else:
         stripe = torch.empty((B, n, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L]
     stripe[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g)
-    rebuilt = torch.empty((B, 1, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L]
+    rebuilt = torch.empty((B, args.rebuilt_rows, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :1, :L]
     survivors = list(range(1, k + 1))
     stream = torch.cuda.current_stream()
+    orig0 = stripe[:, 0].clone() if args.decode_out == "inplace" else None
 
     def step(ev=None):
         if ev is not None:
@@ -578,7 +583,11 @@ def main():
         encode_batch(coder, stripe[:, :k], stripe[:, k:], stream=stream)
         if ev is not None:
             ev[1].record(stream)
-        decode_batch(coder, stripe, survivors, [0], rebuilt, inputs_by_unit=True, stream=stream)
+        if args.decode_out == "inplace":  # rebuild unit 0 into its own slot of the stripe
+            decode_batch(coder, stripe, survivors, [0], stripe, inputs_by_unit=True, outputs_by_unit=True,
+                         stream=stream)
+        else:
+            decode_batch(coder, stripe, survivors, [0], rebuilt, inputs_by_unit=True, stream=stream)
         if ev is not None:
             ev[2].record(stream)
 
@@ -598,7 +607,10 @@ def main():
 
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    ok = bool(torch.equal(rebuilt[:, 0], stripe[:, 0]))
+    if args.decode_out == "inplace":  # unit 0 was rebuilt in place: it must still be the original data
+        ok = bool(torch.equal(stripe[:, 0], orig0))
+    else:
+        ok = bool(torch.equal(rebuilt[:, 0], stripe[:, 0]))
 
     data_bytes_per_rank_step = 2 * B * k * L  # encode k*L + decode k*L survivors, per stripe
     value = world * args.steps * data_bytes_per_rank_step / elapsed / GIB

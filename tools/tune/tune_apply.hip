@@ -544,10 +544,64 @@ static void stream_probe()
     CK(hipFree(sink));
 }
 
+// Encode-shaped XOR probe with a runtime unit stride U: stripe s's unit j at
+// s*6*U + j*U, L <= U bytes used per unit; units 0..3 read, 4..5 written in
+// place.  Asks whether the 64 KiB sweet spot is about the unit
+// stride, and whether padding the stride recovers it for other unit sizes.
+__global__ void unit_stride_kernel(uint8_t* buf, uint64_t U, uint32_t segs, uint32_t total, uint32_t magic,
+                                   uint32_t shift)
+{
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const uint32_t st = static_cast<uint32_t>((static_cast<uint64_t>(idx) * magic) >> shift);
+    const uint64_t off = static_cast<uint64_t>(idx - st * segs) * 16;
+    uint8_t* p = buf + static_cast<uint64_t>(st) * 6 * U + off;
+    uint4 v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint4 x = nt_load(reinterpret_cast<const uint4*>(p + j * U));
+        v = make_uint4(v.x ^ x.x, v.y ^ x.y, v.z ^ x.z, v.w ^ x.w);
+    }
+    nt_store(v, reinterpret_cast<uint4*>(p + 4 * U));
+    nt_store(make_uint4(v.x + 1, v.y, v.z, v.w), reinterpret_cast<uint4*>(p + 5 * U));
+}
+
+static void unit_stride_probe()
+{
+    struct P {
+        uint64_t U, L;
+    };
+    const P ps[] = {{65536, 65536},     {131072, 131072},   {196608, 196608},   {262144, 262144},
+                    {327680, 327680},   {1048576, 1048576}, {1114112, 1048576}, {1179648, 1048576},
+                    {131072, 65536},    {196608, 131072},   {4404224, 4404016}, {4521984, 4404016},
+                    {4456448, 4404016}, {16384, 16384},     {65536, 16384}};
+    for (const P& p : ps) {
+        const uint64_t B = (uint64_t{1} << 30) / (4 * p.L);
+        uint8_t* buf;
+        CK(hipMalloc(&buf, B * 6 * p.U));
+        CK(hipMemset(buf, 7, B * 6 * p.U));
+        const uint32_t segs = static_cast<uint32_t>(p.L / 16), total = static_cast<uint32_t>(B * segs);
+        const Magic mg = make_magic(segs);
+        const dim3 g((total + 255) / 256);
+        const float ms = median_ms([&] {
+            hipLaunchKernelGGL(unit_stride_kernel, g, dim3(256), 0, 0, buf, p.U, segs, total, mg.m, mg.p);
+        });
+        const double moved = 6.0 * B * p.L;
+        std::printf("unit stride %8llu  L %8llu  (stride %6.2f x 64 KiB)  %8.4f ms  %7.1f GB/s  %5.1f%% of 8 TB/s\n",
+                    (unsigned long long)p.U, (unsigned long long)p.L, p.U / 65536.0, ms, moved / (ms * 1e-3) / 1e9,
+                    100.0 * moved / (ms * 1e-3) / 8e12);
+        CK(hipFree(buf));
+    }
+}
+
 int main(int argc, char** argv)
 {
     if (argc > 1 && std::string(argv[1]) == "streams") {
         stream_probe();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "unitstride") {
+        unit_stride_probe();
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "probe") {
