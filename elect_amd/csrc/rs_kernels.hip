@@ -603,8 +603,6 @@ inline int block_for(uint64_t, int) { return AB_BLOCK; }
 #else
 #ifdef AB_BLOCK  // A/B builds (tools/ab_build.sh): one block size for every launch
 inline int block_for(uint64_t, int) { return AB_BLOCK; }
-#elif defined(AB_BLOCK_COEFS)  // A/B: 128 threads from this many coefficients
-inline int block_for(uint64_t len, int coefs) { return (len <= 4096 || coefs >= AB_BLOCK_COEFS) ? 128 : kBlock; }
 #else
 inline int block_for(uint64_t len, int coefs) { return (len <= 4096 || coefs >= 16) ? 128 : kBlock; }
 #endif
