@@ -601,11 +601,7 @@ __global__ __launch_bounds__(kBlock) void hash_reduce(const uint32_t* __restrict
 #ifdef AB_BLOCK  // A/B builds (tools/ab_build.sh): one block size for every launch
 inline int block_for(uint64_t, int) { return AB_BLOCK; }
 #else
-#ifdef AB_BLOCK  // A/B builds (tools/ab_build.sh): one block size for every launch
-inline int block_for(uint64_t, int) { return AB_BLOCK; }
-#else
 inline int block_for(uint64_t len, int coefs) { return (len <= 4096 || coefs >= 16) ? 128 : kBlock; }
-#endif
 #endif
 
 constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches are encodes
