@@ -43,6 +43,10 @@ for step in "$@"; do
             run "ab_s${n}_${SWEEP_CFG:-headline}_$i" 300 python bench.py --config ${SWEEP_CFG:-headline} ${SW[$n]} --no-cpu --no-host --steps ${SWEEP_STEPS:-50} || exit $?
         done; done ;;
     tune) run tune 600 tools/tune/tune_apply || exit $? ;;
+    tuneb2b)  # the two main shapes, launches timed alone vs back to back
+        run tune_alone 300 tools/tune/tune_apply main || exit $?
+        TUNE_B2B=1 run tune_b2b 300 tools/tune/tune_apply main || exit $?
+        TUNE_B2B=1 TUNE_ITERS=400 run tune_b2b_long 300 tools/tune/tune_apply main || exit $? ;;
     envprobe)  # host facts for DESIGN.md: CPU model, ISA-L presence (for a dlopen cross-check)
         { lscpu | grep -E "Model name|^CPU\(s\)|Flags" | cut -c1-200; echo "nproc=$(nproc)";
           echo "isal: $(ldconfig -p 2>/dev/null | grep -ci isal) ldconfig entries";

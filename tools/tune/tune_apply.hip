@@ -318,23 +318,27 @@ struct Runner {
         const uint32_t per_block = BLOCK * U;
         uint32_t grid = (a.total + per_block - 1) / per_block;
         if (GS) grid = std::min<uint32_t>(grid, dev_cus * occ_blocks_per_cu);
-        hipEvent_t e0, e1;
-        CK(hipEventCreate(&e0));
-        CK(hipEventCreate(&e1));
+        // TUNE_B2B=1: launches back to back (one sync at the end), as the product
+        // bench issues them; default: each launch timed alone on an idle GPU.
+        static const bool b2b = std::getenv("TUNE_B2B") && std::atoi(std::getenv("TUNE_B2B")) > 0;
+        std::vector<hipEvent_t> ev(2 * iters);
+        for (auto& e : ev) CK(hipEventCreate(&e));
         std::vector<float> ts;
         for (int i = 0; i < iters; ++i) {
-            CK(hipEventRecord(e0));
+            CK(hipEventRecord(ev[2 * i]));
             hipLaunchKernelGGL((kern<K, R, U, BLOCK, MODE, LD, GS, ORDER, ADJ>), dim3(grid), dim3(BLOCK), 0, 0, a);
-            CK(hipEventRecord(e1));
-            CK(hipEventSynchronize(e1));
+            CK(hipEventRecord(ev[2 * i + 1]));
+            if (!b2b) CK(hipEventSynchronize(ev[2 * i + 1]));
+        }
+        CK(hipDeviceSynchronize());
+        for (int i = 0; i < iters; ++i) {
             float ms = 0;
-            CK(hipEventElapsedTime(&ms, e0, e1));
+            CK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
             ts.push_back(ms);
         }
         CK(hipGetLastError());
         std::sort(ts.begin(), ts.end());
-        CK(hipEventDestroy(e0));
-        CK(hipEventDestroy(e1));
+        for (auto& e : ev) CK(hipEventDestroy(e));
         return ts[ts.size() / 2];
     }
 
@@ -371,7 +375,7 @@ static void sweep(const Shape& s)
 {
     Runner<K, R> rn;
     rn.setup(s);
-    const int it = 25;
+    const int it = std::getenv("TUNE_ITERS") ? std::atoi(std::getenv("TUNE_ITERS")) : 25;
     // reference: U=2, 256, GF, plain
     rn.template time_one<2, 256, kGF, kPlain, false>(0, 3);
     rn.snapshot();
@@ -652,6 +656,11 @@ int main(int argc, char** argv)
                     2.0 * bytes / (ts[12] * 1e-3) / 1e9);
         CK(hipFree(a));
         CK(hipFree(b));
+    }
+    if (argc > 1 && std::string(argv[1]) == "main") {  // the two shapes the product benches most
+        sweep<4, 2>(Shape{"RS(6,4) encode 64KiB", 4, 2, 65536, 4096, 6});
+        sweep<8, 4>(Shape{"RS(12,8) encode 256KiB", 8, 4, 262144, 512, 12});
+        return 0;
     }
     sweep<4, 2>(Shape{"RS(6,4) encode 64KiB", 4, 2, 65536, 4096, 6});
     sweep<4, 1>(Shape{"RS(6,4) decode e=1 64KiB", 4, 1, 65536, 4096, 6});
