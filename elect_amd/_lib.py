@@ -67,6 +67,7 @@ SIGNATURES = [
     ("elect_ec_version", ctypes.c_char_p, []),
     ("elect_ec_strerror", ctypes.c_char_p, [ctypes.c_int]),
     ("elect_ec_device_count", ctypes.c_int, [_ip]),
+    ("elect_ec_unaligned_vector_ok", ctypes.c_int, [_ip]),
     ("elect_ec_set_host_devices", ctypes.c_int, [_ip, ctypes.c_int]),
     ("elect_ec_set_batching", ctypes.c_int, [ctypes.c_int, ctypes.c_uint, ctypes.c_size_t]),
     ("elect_ec_coder_create", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_cp)]),
@@ -130,6 +131,13 @@ def device_count() -> int:
     n = ctypes.c_int(0)
     lib.elect_ec_device_count(ctypes.byref(n))
     return n.value
+
+
+def unaligned_vector_ok() -> bool:
+    """True when misaligned device layouts run the vector kernels (elect_ec.h)."""
+    ok = ctypes.c_int(0)
+    check(lib.elect_ec_unaligned_vector_ok(ctypes.byref(ok)), "unaligned_vector_ok")
+    return bool(ok.value)
 
 
 def set_host_devices(devices) -> None:

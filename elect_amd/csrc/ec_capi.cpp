@@ -109,6 +109,16 @@ const char* elect_ec_strerror(int status)
     }
 }
 
+int elect_ec_unaligned_vector_ok(int* ok)
+{
+    if (!ok) return ELECT_EC_EINVAL;
+    *ok = 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ELECT_EC_ENODEV;
+    *ok = elect::kern::unaligned_vector_ok() ? 1 : 0;
+    return ELECT_EC_OK;
+}
+
 int elect_ec_device_count(int* count)
 {
     if (!count) return ELECT_EC_EINVAL;

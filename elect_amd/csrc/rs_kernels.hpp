@@ -60,6 +60,10 @@ struct ApplyParams {
     // and assigned by hash_reduce with no memset and no atomics; otherwise the
     // launcher seeds the entries (hipMemsetD32Async) and the kernels add.
     bool hash_seed = false;
+    // internal (launch_apply): every column start is 16-byte aligned.  When it
+    // is not, the dwordx4 kernels still run (unaligned vector access, see
+    // unaligned_vector_ok) except gf_apply_lens, whose buffer loads need it.
+    bool aligned16 = true;
 };
 
 // 31^e mod 2^32 (host side of the parity hash).
@@ -87,9 +91,13 @@ struct UpdateParams {
 hipError_t launch_apply(const ApplyParams& p, hipStream_t stream);
 hipError_t launch_update(const UpdateParams& p, hipStream_t stream);
 
-// True when every column start is 16-byte aligned for every stripe, i.e. the
-// dwordx4 fast kernels apply; otherwise the byte-granular kernel runs.
+// True when every column start is 16-byte aligned for every stripe.
 bool apply_is_aligned(const ApplyParams& p);
+
+// True when 16-byte global loads and stores at any byte offset are exact on the
+// current device (checked once per device by a tiny kernel).  Then misaligned
+// layouts run the dwordx4 kernels too; otherwise the byte-granular kernel.
+bool unaligned_vector_ok();
 
 }  // namespace kern
 }  // namespace elect

@@ -74,6 +74,11 @@ const char* elect_ec_version(void);
 const char* elect_ec_strerror(int status);
 /* Number of visible HIP devices (0 with ELECT_EC_ENODEV when none). */
 int elect_ec_device_count(int* count);
+/* *ok = 1 when device-resident layouts whose shard starts are not 16-byte
+ * aligned (any byte offset, e.g. a contiguous [B][k+m][L] batch with L % 16 != 0)
+ * run the vector kernels on the calling thread's current device; 0 when they
+ * fall back to the byte-granular kernel.  Checked once per device. */
+int elect_ec_unaligned_vector_ok(int* ok);
 
 /* Devices for the host-memory calls.  By default a calling thread uses its
  * current HIP device.  With a device list, each calling thread is assigned one

@@ -142,6 +142,8 @@ def test_no_device_fails_loudly():
         c.encode_host([a.ctypes.data for a in d], [a.ctypes.data for a in p], 64)
     # zero-length is a no-op before any device work (JEC/ErasureEncoder.java:41-44)
     assert c.encode_host([a.ctypes.data for a in d], [a.ctypes.data for a in p], 0) == 0
+    with pytest.raises(_lib.ECDeviceError):
+        _lib.unaligned_vector_ok()
 
 
 def test_partition_by_bytes():

@@ -152,25 +152,63 @@ def test_update_in_place_equals_reencode(dev):
     assert torch.equal(par, ref)
 
 
-@pytest.mark.parametrize("shift", [1, 3, 4, 8])
-def test_unaligned_layouts_use_byte_path(dev, oracle, shift):
-    from elect_amd.batch import encode_batch
-    from elect_amd.coder import RSCoder
-    k, m, B, L = 4, 2, 5, 333
-    rng = np.random.default_rng(shift)
-    data = _rand(rng, B, k, L)
-    big = torch.zeros(B * k * L + 64, dtype=torch.uint8, device=dev)
-    view = big[shift:shift + B * k * L].view(B, k, L)
-    view.copy_(_to(dev, data))
-    pbig = torch.zeros(B * m * L + 64, dtype=torch.uint8, device=dev)
-    pv = pbig[shift:shift + B * m * L].view(B, m, L)
-    encode_batch(RSCoder(k, m), view, pv)
-    got = pv.cpu().numpy()
+def _shifted(dev, a, shift):
+    """A device copy of a at a byte offset `shift` from an aligned allocation."""
+    big = torch.zeros(a.size + 64, dtype=torch.uint8, device=dev)
+    view = big[shift:shift + a.size].view(*a.shape)
+    view.copy_(_to(dev, a))
+    return view
+
+
+@pytest.mark.parametrize("shift", [1, 3, 4, 8, 13])
+@pytest.mark.parametrize("L", [333, 4096, 4404020 // 256])
+def test_unaligned_layouts(dev, oracle, shift, L):
+    """Column starts at any byte offset (and strides that are not multiples of
+    16, e.g. ELECT's codeLength in a contiguous [B][k+m][L] layout): the dwordx4
+    kernels run on unaligned addresses (rs_kernels.hip unaligned_vector_ok);
+    encode, decode, update and the fused hash must stay bit-exact."""
+    from elect_amd.batch import decode_batch, encode_batch, encode_batch_hashed, encode_update_batch
+    from elect_amd.coder import RSCoder, java_bytebuffer_hash
+    k, m, B = 4, 2, 5
+    rng = np.random.default_rng(shift * 1000 + L)
+    c = RSCoder(k, m)
     enc = oracle.Encoder(k, m)
+    data = _rand(rng, B, k, L)
+    view = _shifted(dev, data, shift)
+    pv = _shifted(dev, np.zeros((B, m, L), np.uint8), (shift * 5) % 16)
+    hashes = torch.zeros((B, m), dtype=torch.int32, device=dev)
+    encode_batch_hashed(c, view, pv, hashes)
+    got, gh = pv.cpu().numpy(), hashes.cpu().numpy()
+    want = [enc.encode([data[s, j] for j in range(k)]) for s in range(B)]
     for s in range(B):
-        want = enc.encode([data[s, j] for j in range(k)])
         for r in range(m):
-            assert np.array_equal(got[s, r], want[r])
+            assert np.array_equal(got[s, r], want[s][r]), (s, r)
+            assert int(gh[s, r]) == java_bytebuffer_hash(want[s][r])
+    pv2 = _shifted(dev, np.zeros((B, m, L), np.uint8), (shift + 7) % 16)
+    encode_batch(c, view, pv2)
+    assert np.array_equal(pv2.cpu().numpy(), got)
+    # decode from a stripe-resident layout at an odd offset: survivors {1,2,3,4}
+    stripe = np.concatenate([data, got], axis=1)
+    sv = _shifted(dev, stripe, shift)
+    out = _shifted(dev, np.zeros((B, 1, L), np.uint8), (shift + 2) % 16)
+    decode_batch(c, sv, [4, 1, 2, 3], [0], out, inputs_by_unit=True)
+    assert np.array_equal(out.cpu().numpy()[:, 0], data[:, 0])
+    # parity update with every column misaligned
+    new = _rand(rng, B, L)
+    pout = _shifted(dev, np.zeros((B, m, L), np.uint8), (shift + 9) % 16)
+    encode_update_batch(c, 2, view[:, 2], _shifted(dev, new, (shift + 1) % 16), pv, pout)
+    gu = pout.cpu().numpy()
+    for s in range(B):
+        wu = enc.encode_update([data[s, 2], new[s]] + [got[s, r] for r in range(m)], 2)
+        for r in range(m):
+            assert np.array_equal(gu[s, r], wu[r])
+
+
+def test_unaligned_probe_reports_vector_path(dev):
+    """The one-time per-device check behind the unaligned fast path passes on
+    this device (else misaligned layouts would silently take the byte kernel)."""
+    from elect_amd import _lib
+    assert _lib.unaligned_vector_ok()
 
 
 def test_apply_batch_many_rows(dev, oracle):
@@ -305,7 +343,7 @@ def test_encode_padded_host_path(dev, oracle):
         assert np.array_equal(par[r], want[r])
 
 
-def test_padded_unaligned_uses_byte_path(dev, oracle):
+def test_padded_unaligned(dev, oracle):
     from elect_amd.batch import encode_batch_padded
     from elect_amd.coder import RSCoder
     k, m, B, L = 4, 2, 3, 100

@@ -55,6 +55,7 @@ for step in "$@"; do
     probe) run probe 300 tools/tune/tune_apply probe || exit $? ;;
     streams) run streams 300 tools/tune/tune_apply streams || exit $? ;;
     unitstride) run unitstride 300 tools/tune/tune_apply unitstride || exit $? ;;
+    unaligned) run unaligned 120 tools/tune/tune_apply unaligned || exit $? ;;
     multirank)  # rehearse the N>1 flow: 2 ranks sharing the one GPU, gloo handshake
         export ELECT_BENCH_BACKEND=gloo
         run bench_rehearse_2rank 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
