@@ -43,6 +43,7 @@ for step in "$@"; do
             run "ab_s${n}_${SWEEP_CFG:-headline}_$i" 300 python bench.py --config ${SWEEP_CFG:-headline} ${SW[$n]} --no-cpu --no-host --steps ${SWEEP_STEPS:-50} || exit $?
         done; done ;;
     tune) run tune 600 tools/tune/tune_apply || exit $? ;;
+    tunemain) run tune_main 300 tools/tune/tune_apply main || exit $? ;;
     tuneb2b)  # the two main shapes, launches timed alone vs back to back
         run tune_alone 300 tools/tune/tune_apply main || exit $?
         TUNE_B2B=1 run tune_b2b 300 tools/tune/tune_apply main || exit $?

@@ -244,6 +244,79 @@ __global__ __launch_bounds__(BLOCK) void kern(const Args<K, R> a)
     }
 }
 
+// Persistent, software-pipelined variant: a grid of G blocks; iteration t of
+// block b covers segment block t*G + b (grid-stride, so the chip still sweeps
+// memory in the one-shot kernel's order), and every lane issues the loads of
+// iteration t+1 before it computes and stores iteration t.
+template <int K, int R, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void kern_pipe(const Args<K, R> a)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * 8];
+    for (int i = threadIdx.x; i < R * K; i += BLOCK) {
+        const PermTable& t = a.tab[i / K][i % K];
+        tl[i * 8 + 0] = t.t0_lo; tl[i * 8 + 1] = t.t0_hi; tl[i * 8 + 2] = t.t1_lo;
+        tl[i * 8 + 3] = t.t1_hi; tl[i * 8 + 4] = t.t2;
+    }
+    __syncthreads();
+    const uint32_t stride = gridDim.x * BLOCK;
+    uint32_t idx = blockIdx.x * BLOCK + threadIdx.x;
+    auto locate = [&](uint32_t i, uint32_t& st, uint64_t& off) {
+        st = static_cast<uint32_t>((static_cast<uint64_t>(i) * a.magic) >> a.shift);
+        off = static_cast<uint64_t>(i - st * a.segs) * 16;
+    };
+    uint4 cur[K], nxt[K];
+    uint32_t st;
+    uint64_t off;
+    if (idx < a.total) {
+        locate(idx, st, off);
+#pragma unroll
+        for (int j = 0; j < K; ++j) cur[j] = nt_load(reinterpret_cast<const uint4*>(a.sp[j] + st * a.ss[j] + off));
+    }
+    for (; idx < a.total; idx += stride) {
+        uint32_t st_n = 0;
+        uint64_t off_n = 0;
+        const bool more = idx + stride < a.total;
+        if (more) {
+            locate(idx + stride, st_n, off_n);
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                nxt[j] = nt_load(reinterpret_cast<const uint4*>(a.sp[j] + st_n * a.ss[j] + off_n));
+        }
+        uint4 acc[R];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            uint32_t s0[4], s1[4], s2[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t v0 = lane_word(cur[j], w);
+                s0[w] = v0 & 0x07070707u;
+                s1[w] = (v0 >> 3) & 0x07070707u;
+                s2[w] = (v0 >> 6) & 0x03030303u;
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint4 tq = *reinterpret_cast<const uint4*>(&tl[(r * K + j) * 8]);
+                const uint32_t t2 = tl[(r * K + j) * 8 + 4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const uint32_t v = xor3(__builtin_amdgcn_perm(tq.y, tq.x, s0[w]),
+                                            __builtin_amdgcn_perm(tq.w, tq.z, s1[w]),
+                                            __builtin_amdgcn_perm(t2, t2, s2[w]));
+                    set_word(acc[r], w, j == 0 ? v : (lane_word(acc[r], w) ^ v));
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) nt_store(acc[r], reinterpret_cast<uint4*>(a.dp[r] + st * a.ds[r] + off));
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) cur[j] = nxt[j];
+            st = st_n;
+            off = off_n;
+        }
+    }
+}
+
 struct Magic {
     uint32_t m, p;
 };
@@ -342,6 +415,30 @@ struct Runner {
         return ts[ts.size() / 2];
     }
 
+    template <int BLOCK>
+    float time_pipe(int blocks_per_cu, int iters)
+    {
+        const uint32_t grid = std::min<uint32_t>((a.total + BLOCK - 1) / BLOCK, dev_cus * blocks_per_cu);
+        std::vector<float> ts;
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        for (int i = 0; i < iters; ++i) {
+            CK(hipEventRecord(e0));
+            hipLaunchKernelGGL((kern_pipe<K, R, BLOCK>), dim3(grid), dim3(BLOCK), 0, 0, a);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ts.push_back(ms);
+        }
+        CK(hipGetLastError());
+        CK(hipEventDestroy(e0));
+        CK(hipEventDestroy(e1));
+        std::sort(ts.begin(), ts.end());
+        return ts[ts.size() / 2];
+    }
+
     // copy parity region to out_ref (reference output), compare
     void snapshot()
     {
@@ -390,10 +487,11 @@ static void sweep(const Shape& s)
     for (int round = 0; round < 3; ++round) {
         rows.clear();
         rec("U1 b256 nt LDS-tab (product)", rn.template time_one<1, 256, kGF, kNT, false, 2>(0, it), true);
-        rec("U2 b256 nt LDS-tab adjacent", rn.template time_one<2, 256, kGF, kNT, false, 2, true>(0, it), true);
-        rec("U4 b256 nt LDS-tab adjacent", rn.template time_one<4, 256, kGF, kNT, false, 2, true>(0, it), true);
-        rec("U2 b128 nt LDS-tab adjacent", rn.template time_one<2, 128, kGF, kNT, false, 2, true>(0, it), true);
-        rec("U2 b256 nt LDS-tab 4KiB apart", rn.template time_one<2, 256, kGF, kNT, false, 2>(0, it), true);
+        rec("pipelined b256 x2/CU", rn.template time_pipe<256>(2, it), true);
+        rec("pipelined b256 x4/CU", rn.template time_pipe<256>(4, it), true);
+        rec("pipelined b256 x8/CU", rn.template time_pipe<256>(8, it), true);
+        rec("pipelined b128 x8/CU", rn.template time_pipe<128>(8, it), true);
+        rec("pipelined b256 x16/CU", rn.template time_pipe<256>(16, it), true);
         rec("U1 XOR-only nt both", rn.template time_one<1, 256, kXor, kNT, false>(0, it), false);
         rec("U2 XOR-only nt both adjacent", rn.template time_one<2, 256, kXor, kNT, false, 0, true>(0, it), false);
         // restore reference output for later variants' checks
@@ -726,6 +824,8 @@ int main(int argc, char** argv)
     if (argc > 1 && std::string(argv[1]) == "main") {  // the two shapes the product benches most
         sweep<4, 2>(Shape{"RS(6,4) encode 64KiB", 4, 2, 65536, 4096, 6});
         sweep<8, 4>(Shape{"RS(12,8) encode 256KiB", 8, 4, 262144, 512, 12});
+        sweep<4, 1>(Shape{"RS(6,4) decode e=1 64KiB", 4, 1, 65536, 4096, 6});
+        sweep<4, 2>(Shape{"RS(6,4) encode 1MiB", 4, 2, 1048576, 256, 6});
         return 0;
     }
     sweep<4, 2>(Shape{"RS(6,4) encode 64KiB", 4, 2, 65536, 4096, 6});
