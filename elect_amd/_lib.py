@@ -83,6 +83,10 @@ SIGNATURES = [
                                               ctypes.c_size_t]),
     ("elect_ec_encode_hashed", ctypes.c_int, [_cp, _u8pp, _u8pp, ctypes.c_size_t,
                                               ctypes.POINTER(ctypes.c_int32)]),
+    ("elect_ec_encode_ex", ctypes.c_int, [_cp, _u8pp, ctypes.POINTER(ctypes.c_size_t), _u8pp, ctypes.c_size_t,
+                                          ctypes.POINTER(ctypes.c_int32)]),
+    ("elect_ec_encode_update_ex", ctypes.c_int, [_cp, _u8pp, ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
+                                                 _u8pp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32)]),
     ("elect_ec_decode", ctypes.c_int, [_cp, _u8pp, _ip, _ip, ctypes.c_int, _u8pp, ctypes.c_size_t,
                                        ctypes.c_int]),
     ("elect_ec_encode_batch", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, Shards, Shards, _cp]),
@@ -94,6 +98,10 @@ SIGNATURES = [
                                                     _cp, _cp]),
     ("elect_ec_encode_update_batch", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                                                     ColumnT, ColumnT, Shards, Shards, _cp]),
+    ("elect_ec_encode_batch_ex", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, Shards, _cp, Shards,
+                                                _cp, _cp]),
+    ("elect_ec_encode_update_batch_ex", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                                                       ColumnT, ColumnT, _cp, Shards, Shards, _cp, _cp]),
     ("elect_ec_apply_batch", ctypes.c_int, [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
                                             ctypes.c_size_t, ctypes.POINTER(ColumnT),
                                             ctypes.POINTER(ColumnT), _cp]),

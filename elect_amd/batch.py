@@ -93,6 +93,51 @@ def encode_update_batch(coder: RSCoder, target: int, old: torch.Tensor, new: tor
           "encode_update_batch")
 
 
+def _lengths(lengths, B: int, n: int, device) -> int:
+    if lengths is None:
+        return None
+    if lengths.shape != (B, n) or lengths.dtype not in (torch.int32, torch.uint32) or \
+            not lengths.is_contiguous() or lengths.device != device:
+        raise ValueError(f"lengths must be a contiguous int32 [{B}, {n}] tensor on the data's device")
+    return lengths.data_ptr()
+
+
+def _hashes(hashes, B: int, m: int, device) -> int:
+    if hashes is None:
+        return None
+    if hashes.shape != (B, m) or hashes.dtype != torch.int32 or not hashes.is_contiguous() or \
+            hashes.device != device:
+        raise ValueError(f"hashes must be a contiguous int32 [{B}, {m}] tensor on the data's device")
+    return hashes.data_ptr()
+
+
+def encode_batch_ex(coder: RSCoder, data: torch.Tensor, parity: torch.Tensor, lengths=None, hashes=None,
+                    stream=None) -> None:
+    """ELECT's coding-node encode step in one launch (ECMessageVerbHandler.java:283-329):
+    data[s, j] holds lengths[s, j] content bytes (None: all full; the rest reads as zero),
+    and hashes[s, r] (None: not wanted) receives parity[s, r]'s ByteBuffer.hashCode()."""
+    B, k, L = data.shape
+    if k != coder.k or parity.shape != (B, coder.m, L):
+        raise ValueError(f"shape mismatch: data {tuple(data.shape)} parity {tuple(parity.shape)}")
+    check(lib.elect_ec_encode_batch_ex(coder.handle, L, B, _shards(data), _lengths(lengths, B, k, data.device),
+                                       _shards(parity), _hashes(hashes, B, coder.m, data.device), _stream(stream)),
+          "encode_batch_ex")
+
+
+def encode_update_batch_ex(coder: RSCoder, target: int, old: torch.Tensor, new: torch.Tensor,
+                           parity_in: torch.Tensor, parity_out: torch.Tensor, lengths=None, hashes=None,
+                           stream=None) -> None:
+    """ELECT's parity-update step in one launch (ECParityUpdateVerbHandler.java:634-699):
+    old[s] / new[s] hold lengths[s, 0] / lengths[s, 1] content bytes (None: full), the
+    new parity goes to parity_out (may be parity_in) and its hashCode() to hashes[s, r]."""
+    B, L = old.shape
+    check(lib.elect_ec_encode_update_batch_ex(coder.handle, L, B, target, _column(old), _column(new),
+                                              _lengths(lengths, B, 2, old.device), _shards(parity_in),
+                                              _shards(parity_out), _hashes(hashes, B, coder.m, old.device),
+                                              _stream(stream)),
+          "encode_update_batch_ex")
+
+
 def apply_batch(coef: np.ndarray, src, dst, stream=None) -> None:
     """dst[r] = XOR_j coef[r, j] * src[j] over [B, L] column tensors."""
     coef = np.ascontiguousarray(coef, np.uint8)

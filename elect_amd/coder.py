@@ -255,6 +255,33 @@ class RSCoder:
         return check(lib.elect_ec_encode_padded(self.handle, ptr_array(addrs), lens, ptr_array(parity_addrs),
                                                 length), "encode_padded")
 
+    def encode_ex_host(self, data_addrs, parity_addrs, length: int, data_lengths=None, hashed: bool = False):
+        """ELECT's whole coding-node encode step (ECMessageVerbHandler.java:283-329): zero fill
+        to `length` (data_lengths; None address for an empty unit), encode, and (hashed) each
+        parity unit's ByteBuffer.hashCode().  Returns the hashes, or None."""
+        lens = None
+        if data_lengths is not None:
+            lens = (_lib.ctypes.c_size_t * len(data_lengths))(*[int(x) for x in data_lengths])
+        h = (_lib.ctypes.c_int32 * self.m)() if hashed else None
+        addrs = [a if a is not None else 0 for a in data_addrs]
+        check(lib.elect_ec_encode_ex(self.handle, ptr_array(addrs), lens, ptr_array(parity_addrs), length, h),
+              "encode_ex")
+        return list(h) if hashed else None
+
+    def encode_update_ex_host(self, in_addrs, target: int, out_addrs, length: int, old_new_lengths=None,
+                              hashed: bool = False):
+        """ELECT's whole parity-update step (ECParityUpdateVerbHandler.java:634-699): old/new
+        zero filled to `length` (old_new_lengths), P' = P ^ E[k+r][target]*(old^new), and
+        (hashed) each new parity unit's ByteBuffer.hashCode().  Returns the hashes, or None."""
+        lens = None
+        if old_new_lengths is not None:
+            lens = (_lib.ctypes.c_size_t * 2)(*[int(x) for x in old_new_lengths])
+        h = (_lib.ctypes.c_int32 * self.m)() if hashed else None
+        addrs = [a if a is not None else 0 for a in in_addrs]
+        check(lib.elect_ec_encode_update_ex(self.handle, ptr_array(addrs), lens, target, ptr_array(out_addrs),
+                                            length, h), "encode_update_ex")
+        return list(h) if hashed else None
+
     def encode_update_host(self, in_addrs, target: int, out_addrs, length: int) -> int:
         return check(lib.elect_ec_encode_update(self.handle, ptr_array(in_addrs), target,
                                                 ptr_array(out_addrs), length), "encodeUpdate")

@@ -196,26 +196,13 @@ int elect_ec_encode(const elect_ec_coder* coder, const unsigned char* const* dat
     return run_host(op, chunk_size);
 }
 
-int elect_ec_encode_padded(const elect_ec_coder* coder, const unsigned char* const* data_units,
-                           const size_t* data_lengths, unsigned char* const* parity_units, size_t chunk_size)
+int elect_ec_encode_ex(const elect_ec_coder* coder, const unsigned char* const* data_units,
+                       const size_t* data_lengths, unsigned char* const* parity_units, size_t chunk_size,
+                       int32_t* hashes)
 {
-    if (!valid_coder(coder) || !data_units || !data_lengths || !parity_units) return ELECT_EC_EINVAL;
-    if (chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
-    HostOp op;
-    op.cols = coder->k;
-    op.rows = coder->m;
-    op.in = data_units;
-    op.out = parity_units;
-    op.lens = data_lengths;
-    for (int r = 0; r < coder->m; ++r) std::memcpy(op.coef + r * op.cols, parity_row(coder, r), coder->k);
-    return run_host(op, chunk_size);
-}
-
-int elect_ec_encode_hashed(const elect_ec_coder* coder, const unsigned char* const* data_units,
-                           unsigned char* const* parity_units, size_t chunk_size, int32_t* hashes)
-{
-    if (!valid_coder(coder) || !data_units || !parity_units || !hashes) return ELECT_EC_EINVAL;
-    if (chunk_size == 0) {  // hashCode of an empty buffer is 1
+    if (!valid_coder(coder) || !data_units || !parity_units) return ELECT_EC_EINVAL;
+    if (data_lengths && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
+    if (hashes && chunk_size == 0) {  // hashCode of an empty buffer is 1
         for (int r = 0; r < coder->m; ++r) hashes[r] = 1;
         return ELECT_EC_OK;
     }
@@ -224,9 +211,24 @@ int elect_ec_encode_hashed(const elect_ec_coder* coder, const unsigned char* con
     op.rows = coder->m;
     op.in = data_units;
     op.out = parity_units;
+    op.lens = data_lengths;
     op.hashes = hashes;
     for (int r = 0; r < coder->m; ++r) std::memcpy(op.coef + r * op.cols, parity_row(coder, r), coder->k);
     return run_host(op, chunk_size);
+}
+
+int elect_ec_encode_padded(const elect_ec_coder* coder, const unsigned char* const* data_units,
+                           const size_t* data_lengths, unsigned char* const* parity_units, size_t chunk_size)
+{
+    if (!data_lengths) return ELECT_EC_EINVAL;
+    return elect_ec_encode_ex(coder, data_units, data_lengths, parity_units, chunk_size, nullptr);
+}
+
+int elect_ec_encode_hashed(const elect_ec_coder* coder, const unsigned char* const* data_units,
+                           unsigned char* const* parity_units, size_t chunk_size, int32_t* hashes)
+{
+    if (!hashes) return ELECT_EC_EINVAL;
+    return elect_ec_encode_ex(coder, data_units, nullptr, parity_units, chunk_size, hashes);
 }
 
 int elect_ec_encode_update(const elect_ec_coder* coder, const unsigned char* const* old_new_parity,
@@ -241,6 +243,44 @@ int elect_ec_encode_update(const elect_ec_coder* coder, const unsigned char* con
     op.in = old_new_parity;
     op.out = new_parity_units;
     for (int r = 0; r < coder->m; ++r) op.coef[r] = parity_row(coder, r)[target_data_index];
+    return run_host(op, chunk_size);
+}
+
+int elect_ec_encode_update_ex(const elect_ec_coder* coder, const unsigned char* const* old_new_parity,
+                              const size_t* old_new_lengths, int target_data_index,
+                              unsigned char* const* new_parity_units, size_t chunk_size, int32_t* hashes)
+{
+    if (!valid_coder(coder) || !old_new_parity || !new_parity_units) return ELECT_EC_EINVAL;
+    if (target_data_index < 0 || target_data_index >= coder->k) return ELECT_EC_EINVAL;
+    if (!old_new_lengths && !hashes)
+        return elect_ec_encode_update(coder, old_new_parity, target_data_index, new_parity_units, chunk_size);
+    if (hashes && 2 + coder->m > ELECT_EC_MAX_DATA_UNITS) return ELECT_EC_EINVAL;
+    if (old_new_lengths && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
+    if (hashes && chunk_size == 0) {
+        for (int r = 0; r < coder->m; ++r) hashes[r] = 1;
+        return ELECT_EC_OK;
+    }
+    // The update as a (2+m)-column product [c_r, c_r, e_r] over [old, new, P...]:
+    // the padded and hashed encode machinery then serves it unchanged.
+    HostOp op;
+    op.cols = 2 + coder->m;
+    op.rows = coder->m;
+    op.in = old_new_parity;
+    op.out = new_parity_units;
+    size_t lens[elect::kern::kMaxCols] = {};
+    if (old_new_lengths) {
+        lens[0] = old_new_lengths[0];
+        lens[1] = old_new_lengths[1];
+        for (int r = 0; r < coder->m; ++r) lens[2 + r] = chunk_size;
+        op.lens = lens;
+    }
+    op.hashes = hashes;
+    for (int r = 0; r < coder->m; ++r) {
+        const uint8_t c = parity_row(coder, r)[target_data_index];
+        op.coef[r * op.cols + 0] = c;
+        op.coef[r * op.cols + 1] = c;
+        op.coef[r * op.cols + 2 + r] = 1;
+    }
     return run_host(op, chunk_size);
 }
 
@@ -282,21 +322,28 @@ int elect_ec_encode_batch(const elect_ec_coder* coder, size_t chunk_size, size_t
     return map_hip(elect::kern::launch_apply(p, as_stream(stream)));
 }
 
-int elect_ec_encode_batch_padded(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
-                                 elect_ec_shards data, const uint32_t* data_lengths, elect_ec_shards parity,
-                                 void* stream)
+int elect_ec_encode_batch_ex(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                             elect_ec_shards data, const uint32_t* d_data_lengths, elect_ec_shards parity,
+                             int32_t* d_hashes, void* stream)
 {
-    if (!valid_coder(coder) || !data_lengths) return ELECT_EC_EINVAL;
-    if (chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
-    if (chunk_size == 0 || num_stripes == 0) return ELECT_EC_OK;
-    if (!data.base || !parity.base) return ELECT_EC_EINVAL;
+    if (!valid_coder(coder)) return ELECT_EC_EINVAL;
+    if (d_data_lengths && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
+    if (num_stripes == 0 || (chunk_size == 0 && !d_hashes)) return ELECT_EC_OK;
+    if (chunk_size > 0 && (!data.base || !parity.base)) return ELECT_EC_EINVAL;
     ApplyParams p;
     p.len = chunk_size;
     p.stripes = num_stripes;
     p.cols = coder->k;
     p.rows = coder->m;
-    p.padded = true;
-    p.lens = data_lengths;
+    if (d_data_lengths) {
+        p.padded = true;
+        p.lens = d_data_lengths;
+    }
+    if (d_hashes) {
+        p.hash_seed = true;  // the launcher produces 31^len + sum (no separate memset where it can)
+        p.hashes = d_hashes;
+        p.hash_stride = static_cast<uint32_t>(coder->m);
+    }
     for (int j = 0; j < p.cols; ++j) p.src[j] = col(data.base, data.stripe_stride, j * data.shard_stride);
     for (int r = 0; r < p.rows; ++r) {
         p.dst[r] = col(parity.base, parity.stripe_stride, r * parity.shard_stride);
@@ -305,26 +352,19 @@ int elect_ec_encode_batch_padded(const elect_ec_coder* coder, size_t chunk_size,
     return map_hip(elect::kern::launch_apply(p, as_stream(stream)));
 }
 
+int elect_ec_encode_batch_padded(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                                 elect_ec_shards data, const uint32_t* data_lengths, elect_ec_shards parity,
+                                 void* stream)
+{
+    if (!data_lengths) return ELECT_EC_EINVAL;
+    return elect_ec_encode_batch_ex(coder, chunk_size, num_stripes, data, data_lengths, parity, nullptr, stream);
+}
+
 int elect_ec_encode_batch_hashed(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
                                  elect_ec_shards data, elect_ec_shards parity, int32_t* d_hashes, void* stream)
 {
-    if (!valid_coder(coder) || !d_hashes) return ELECT_EC_EINVAL;
-    if (num_stripes == 0) return ELECT_EC_OK;
-    if (chunk_size > 0 && (!data.base || !parity.base)) return ELECT_EC_EINVAL;
-    ApplyParams p;
-    p.hash_seed = true;  // the launcher produces 31^len + sum (no separate memset where it can)
-    p.len = chunk_size;
-    p.stripes = num_stripes;
-    p.cols = coder->k;
-    p.rows = coder->m;
-    p.hashes = d_hashes;
-    p.hash_stride = static_cast<uint32_t>(coder->m);
-    for (int j = 0; j < p.cols; ++j) p.src[j] = col(data.base, data.stripe_stride, j * data.shard_stride);
-    for (int r = 0; r < p.rows; ++r) {
-        p.dst[r] = col(parity.base, parity.stripe_stride, r * parity.shard_stride);
-        std::memcpy(p.coef + r * p.cols, parity_row(coder, r), coder->k);
-    }
-    return map_hip(elect::kern::launch_apply(p, as_stream(stream)));
+    if (!d_hashes) return ELECT_EC_EINVAL;
+    return elect_ec_encode_batch_ex(coder, chunk_size, num_stripes, data, nullptr, parity, d_hashes, stream);
 }
 
 int elect_ec_decode_batch(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
@@ -372,6 +412,51 @@ int elect_ec_encode_update_batch(const elect_ec_coder* coder, size_t chunk_size,
         p.coef[r] = parity_row(coder, r)[target_data_index];
     }
     return map_hip(elect::kern::launch_update(p, as_stream(stream)));
+}
+
+int elect_ec_encode_update_batch_ex(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                                    int target_data_index, elect_ec_column old_data, elect_ec_column new_data,
+                                    const uint32_t* d_old_new_lengths, elect_ec_shards parity_in,
+                                    elect_ec_shards parity_out, int32_t* d_hashes, void* stream)
+{
+    if (!valid_coder(coder) || target_data_index < 0 || target_data_index >= coder->k) return ELECT_EC_EINVAL;
+    if (!d_old_new_lengths && !d_hashes)
+        return elect_ec_encode_update_batch(coder, chunk_size, num_stripes, target_data_index, old_data, new_data,
+                                            parity_in, parity_out, stream);
+    if (d_hashes && 2 + coder->m > ELECT_EC_MAX_DATA_UNITS) return ELECT_EC_EINVAL;
+    if (d_old_new_lengths && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
+    if (num_stripes == 0 || (chunk_size == 0 && !d_hashes)) return ELECT_EC_OK;
+    if (chunk_size > 0 && (!old_data.ptr || !new_data.ptr || !parity_in.base || !parity_out.base))
+        return ELECT_EC_EINVAL;
+    // [c_r, c_r, e_r] over [old, new, P...] (see elect_ec_encode_update_ex).
+    ApplyParams p;
+    p.len = chunk_size;
+    p.stripes = num_stripes;
+    p.cols = 2 + coder->m;
+    p.rows = coder->m;
+    p.src[0] = col(old_data.ptr, old_data.stripe_stride, 0);
+    p.src[1] = col(new_data.ptr, new_data.stripe_stride, 0);
+    for (int r = 0; r < p.rows; ++r) {
+        p.src[2 + r] = col(parity_in.base, parity_in.stripe_stride, r * parity_in.shard_stride);
+        p.dst[r] = col(parity_out.base, parity_out.stripe_stride, r * parity_out.shard_stride);
+        const uint8_t c = parity_row(coder, r)[target_data_index];
+        p.coef[r * p.cols + 0] = c;
+        p.coef[r * p.cols + 1] = c;
+        p.coef[r * p.cols + 2 + r] = 1;
+    }
+    if (d_old_new_lengths) {  // old/new padded; the old parity is full length
+        p.padded = true;
+        p.lens = d_old_new_lengths;
+        p.lens_cols = 2;
+        p.lens_stride = 2;
+        for (int r = 0; r < p.rows; ++r) p.clen[2 + r] = static_cast<uint32_t>(chunk_size);
+    }
+    if (d_hashes) {
+        p.hash_seed = true;
+        p.hashes = d_hashes;
+        p.hash_stride = static_cast<uint32_t>(coder->m);
+    }
+    return map_hip(elect::kern::launch_apply(p, as_stream(stream)));
 }
 
 int elect_ec_apply_batch(const unsigned char* coef, int rows, int cols, size_t chunk_size, size_t num_stripes,

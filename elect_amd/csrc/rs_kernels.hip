@@ -249,8 +249,9 @@ struct FastArgs {
     uint32_t shift;
     // padded launches only
     uint64_t len;            // bytes per shard (the last segment may be partial)
-    const uint32_t* lens;    // [stripe][lstride] content lengths, or null -> clen
+    const uint32_t* lens;    // [stripe][lstride] content lengths of columns < lcols, or null -> clen
     uint32_t lstride;
+    uint32_t lcols;          // columns >= lcols hold clen[j] valid bytes
     uint32_t clen[K];
     int32_t* hashes;        // optional parity hashes, [stripe][hstride] (row r at +r)
     uint32_t hstride;
@@ -343,7 +344,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         uniform = s0 == s1;
         const uint32_t* l = a.lens + static_cast<uint64_t>(s0) * a.lstride;
 #pragma unroll
-        for (int j = 0; j < K; ++j) sl[j] = __builtin_amdgcn_readfirstlane(l[j]);
+        for (int j = 0; j < K; ++j) sl[j] = j < a.lcols ? __builtin_amdgcn_readfirstlane(l[j]) : a.clen[j];
     }
 
     stage_tables(a, tl);
@@ -364,7 +365,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         } else {  // all lengths first: vmcnt is in order, so interleaving would serialise
             const uint32_t* l = a.lens + static_cast<uint64_t>(stripe) * a.lstride;
 #pragma unroll
-            for (int j = 0; j < K; ++j) valid[j] = l[j];
+            for (int j = 0; j < K; ++j) valid[j] = j < a.lcols ? l[j] : a.clen[j];
         }
         // Full segments first (no loads at all past a column's content length),
         // then the rare straddling segment into separate registers, so no load
@@ -479,7 +480,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
         uniform = s0 == stripe_of(min(first + 64u * U - 1u, a.total - 1u));
         const uint32_t* l = a.lens + static_cast<uint64_t>(s0) * a.lstride;
 #pragma unroll
-        for (int j = 0; j < K; ++j) sl[j] = __builtin_amdgcn_readfirstlane(l[j]);
+        for (int j = 0; j < K; ++j) sl[j] = j < a.lcols ? __builtin_amdgcn_readfirstlane(l[j]) : a.clen[j];
     }
     stage_tables(a, tl);
     if (first >= a.total) return;
@@ -540,7 +541,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
         const uint32_t* l = a.lens + static_cast<uint64_t>(stripe) * a.lstride;
         uint32_t valid[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) valid[j] = l[j];
+        for (int j = 0; j < K; ++j) valid[j] = j < a.lcols ? l[j] : a.clen[j];
         uint4 x[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
@@ -620,7 +621,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     a.magic = mg.m;
     a.shift = mg.p;
     a.len = p.len;
-    a.lstride = static_cast<uint32_t>(p.cols);
+    a.lstride = p.lens_stride ? p.lens_stride : static_cast<uint32_t>(p.cols);
+    a.lcols = static_cast<uint32_t>(p.lens_cols ? p.lens_cols : p.cols);
     for (int j = 0; j < K; ++j) a.clen[j] = p.clen[j];
     a.hstride = p.hash_stride;
     a.hpow = pow31(p.hash_base);
@@ -639,7 +641,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             a.dp[r] = const_cast<uint8_t*>(p.dst[r0 + r].ptr) + s0 * p.dst[r0 + r].stride;
             a.ds[r] = p.dst[r0 + r].stride;
         }
-        a.lens = p.lens ? p.lens + s0 * p.cols : nullptr;
+        a.lens = p.lens ? p.lens + s0 * a.lstride : nullptr;
         a.hashes = p.hashes ? p.hashes + s0 * p.hash_stride + r0 : nullptr;
         a.total = static_cast<uint32_t>(ns * segs64);
         a.hpart = nullptr;
@@ -723,7 +725,9 @@ struct GenericArgs {
     int cols;
     int rows;
     uint8_t coef[kMaxRows * kMaxCols];
-    const uint32_t* lens;  // padded: [stripe][cols] content lengths, or null -> clen
+    const uint32_t* lens;  // padded: [stripe][lstride] content lengths of columns < lcols, or null -> clen
+    uint32_t lstride;
+    int lcols;
     uint32_t clen[kMaxCols];
     int padded;
     uint32_t col_base;     // byte offset of this launch window inside the shard
@@ -746,7 +750,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_bytes(const GenericArgs a)
     for (int j = 0; j < a.cols; ++j) {
         uint8_t v = 0;
         if (a.padded) {
-            const uint32_t valid = a.lens ? a.lens[static_cast<uint64_t>(s) * a.cols + j] : a.clen[j];
+            const uint32_t valid = a.lens && j < a.lcols ? a.lens[static_cast<uint64_t>(s) * a.lstride + j] : a.clen[j];
             if (a.col_base + i < valid) v = a.sp[j][s * a.ss[j] + i];
         } else {
             v = a.sp[j][s * a.ss[j] + i];
@@ -790,6 +794,8 @@ hipError_t launch_bytes(const ApplyParams& p, hipStream_t stream)
     a.rows = p.rows;
     std::copy(p.coef, p.coef + kMaxRows * kMaxCols, a.coef);
     a.padded = p.padded ? 1 : 0;
+    a.lstride = p.lens_stride ? p.lens_stride : static_cast<uint32_t>(p.cols);
+    a.lcols = p.lens_cols ? p.lens_cols : p.cols;
     std::copy(p.clen, p.clen + kMaxCols, a.clen);
     a.col_base = p.padded ? p.col_base : 0;
     a.hstride = p.hash_stride;
@@ -808,7 +814,7 @@ hipError_t launch_bytes(const ApplyParams& p, hipStream_t stream)
             a.dp[r] = const_cast<uint8_t*>(p.dst[r].ptr) + s0 * p.dst[r].stride;
             a.ds[r] = p.dst[r].stride;
         }
-        a.lens = p.lens ? p.lens + s0 * p.cols : nullptr;
+        a.lens = p.lens ? p.lens + s0 * a.lstride : nullptr;
         a.hashes = p.hashes ? p.hashes + s0 * p.hash_stride : nullptr;
         a.total = static_cast<uint32_t>(ns * p.len);
         const uint32_t grid = (a.total + kBlock - 1) / kBlock;
@@ -1013,7 +1019,7 @@ hipError_t launch_apply(const ApplyParams& p_in, hipStream_t stream)
     if (p.len == 0) return hipSuccess;
     if (p.padded) {
         for (int j = 0; j < p.cols; ++j)
-            if (!p.lens && p.clen[j] > p.len) return hipErrorInvalidValue;
+            if ((!p.lens || (p.lens_cols && j >= p.lens_cols)) && p.clen[j] > p.len) return hipErrorInvalidValue;
         if (!vec || p.cols > kMaxPadCols) return launch_bytes(p, stream);
         for (int r0 = 0; r0 < p.rows; r0 += kFastRows) {
             const int nr = std::min(kFastRows, p.rows - r0);

@@ -44,6 +44,12 @@ struct ApplyParams {
     bool padded = false;
     const uint32_t* lens = nullptr;
     uint32_t clen[kMaxCols] = {};
+    // lens holds lens_stride entries per stripe (0: cols) for the first
+    // lens_cols columns (0: all); the other columns hold clen[j] valid bytes.
+    // ELECT's parity update pads old/new SSTables but not the old parity
+    // (ECParityUpdateVerbHandler.java:643-663).
+    int lens_cols = 0;
+    uint32_t lens_stride = 0;
     uint32_t col_base = 0;  // internal: byte offset of a launch window inside the shard
     // Optional java.nio.ByteBuffer.hashCode() of every output row (ELECT names
     // parity by it, ECMessageVerbHandler.java:326-329):

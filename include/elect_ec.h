@@ -161,6 +161,26 @@ int elect_ec_encode_padded(const elect_ec_coder* coder, const unsigned char* con
 int elect_ec_encode_hashed(const elect_ec_coder* coder, const unsigned char* const* data_units,
                            unsigned char* const* parity_units, size_t chunk_size, int32_t* hashes);
 
+/* ---- ELECT's two coding-node steps, each fused into one pass (host memory) ----
+ * encode_ex is the whole redundancy-transition encode of
+ * JEC/net/ECMessageVerbHandler.java:283-329: zero fill of each SSTable up to
+ * codeLength (data_lengths, NULL = all full), encode, and the parity
+ * hashCode() values that name the parity blocks (hashes, NULL = not wanted).
+ * encode_padded / encode_hashed are the two halves of it. */
+int elect_ec_encode_ex(const elect_ec_coder* coder, const unsigned char* const* data_units,
+                       const size_t* data_lengths, unsigned char* const* parity_units,
+                       size_t chunk_size, int32_t* hashes);
+/* encode_update_ex is the whole parity update of ECParityUpdateVerbHandler.java:
+ * 634-699: old and new SSTable contents zero filled up to codeLength
+ * (old_new_lengths[0..1], NULL = both full; a NULL data pointer is allowed for a
+ * zero length), P'[r] = P[r] ^ E[k+r][target] * (old ^ new) (ec_encode_data_update,
+ * EC/erasure_coder.c:100-142), and hashCode() of every new parity unit (hashes,
+ * NULL = not wanted; needs m <= 8).  Inputs [old, new, P0..Pm-1] as
+ * elect_ec_encode_update; outputs may alias the old parity. */
+int elect_ec_encode_update_ex(const elect_ec_coder* coder, const unsigned char* const* old_new_parity,
+                              const size_t* old_new_lengths, int target_data_index,
+                              unsigned char* const* new_parity_units, size_t chunk_size, int32_t* hashes);
+
 /* ---- device resident, batched, stream ordered ----
  * Many stripes per launch.  All pointers are device pointers on the calling
  * thread's current device; the call only enqueues work on `stream`.  16-byte
@@ -190,6 +210,19 @@ int elect_ec_encode_update_batch(const elect_ec_coder* coder, size_t chunk_size,
                                  elect_ec_column old_data, elect_ec_column new_data,
                                  elect_ec_shards parity_in, elect_ec_shards parity_out,
                                  void* stream);
+/* Device-resident forms of encode_ex / encode_update_ex: one launch per call.
+ * d_data_lengths: DEVICE uint32 [num_stripes][k] (NULL = all full);
+ * d_old_new_lengths: DEVICE uint32 [num_stripes][2], old then new content
+ * length (NULL = both full); d_hashes: DEVICE int32 [num_stripes][m], overwritten
+ * (NULL = not wanted; the update needs m <= 8 for it).  parity_out may equal
+ * parity_in (in place). */
+int elect_ec_encode_batch_ex(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                             elect_ec_shards data, const uint32_t* d_data_lengths, elect_ec_shards parity,
+                             int32_t* d_hashes, void* stream);
+int elect_ec_encode_update_batch_ex(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                                    int target_data_index, elect_ec_column old_data, elect_ec_column new_data,
+                                    const uint32_t* d_old_new_lengths, elect_ec_shards parity_in,
+                                    elect_ec_shards parity_out, int32_t* d_hashes, void* stream);
 /* General product dst[r] = XOR_j coef[r*cols+j] * src[j], rows, cols <= 16. */
 int elect_ec_apply_batch(const unsigned char* coef, int rows, int cols, size_t chunk_size,
                          size_t num_stripes, const elect_ec_column* src,

@@ -567,3 +567,12 @@ void oracle_fill_splitmix(uint64_t seed, unsigned char* buf, size_t len)
             buf[i + (size_t)b] = (unsigned char)(z >> (8 * b));
     }
 }
+
+/* JDK ByteBuffer.hashCode() loop (see ec_oracle.h); unsigned arithmetic is the
+ * int32 wrap-around Java defines. */
+int32_t oracle_java_bytebuffer_hashcode(const unsigned char* b, size_t n)
+{
+    uint32_t h = 1;
+    for (size_t i = n; i-- > 0;) h = 31u * h + (uint32_t)(int32_t)(signed char)b[i];
+    return (int32_t)h;
+}

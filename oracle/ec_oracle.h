@@ -101,6 +101,14 @@ double oracle_batch_apply(int level, int threads, const unsigned char* coef, int
                           const unsigned char* src, size_t src_stripe, const int64_t* src_col_off,
                           unsigned char* dst, size_t dst_stripe, const int64_t* dst_row_off);
 
+/* ---- ELECT's callers around the coder (JEC/net) ----
+ * java.nio.ByteBuffer.hashCode() as the JDK specifies it, over [0, n) of a
+ * buffer at position 0 / limit n: h = 1; for (i = n-1; i >= 0; i--)
+ * h = 31*h + (int)(byte)b[i]; int32 wrap-around.  ELECT names every parity
+ * block by it (ECMessageVerbHandler.java:326-329, ECParityUpdateVerbHandler.java:
+ * 696-699).  A plain Horner loop, not the closed form the product uses. */
+int32_t oracle_java_bytebuffer_hashcode(const unsigned char* b, size_t n);
+
 /* splitmix64 byte stream (little-endian words) used to make fixture inputs. */
 void oracle_fill_splitmix(uint64_t seed, unsigned char* buf, size_t len);
 

@@ -69,6 +69,8 @@ def lib():
                                          ctypes.c_void_p, ctypes.c_size_t,
                                          ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p,
                                          ctypes.c_size_t, ctypes.POINTER(ctypes.c_int64)]
+        L.oracle_java_bytebuffer_hashcode.restype = ctypes.c_int32
+        L.oracle_java_bytebuffer_hashcode.argtypes = [u8p, ctypes.c_size_t]
         L.oracle_fill_splitmix.argtypes = [ctypes.c_uint64, u8p, ctypes.c_size_t]
         _lib = L
     return _lib
@@ -220,4 +222,19 @@ def batch_apply(coef: np.ndarray, src: np.ndarray, src_stripe: int, src_col_off,
 def splitmix_bytes(seed: int, n: int) -> np.ndarray:
     out = np.empty(n, np.uint8)
     lib().oracle_fill_splitmix(ctypes.c_uint64(seed), _p(out), n)
+    return out
+
+
+def java_hashcode(b) -> int:
+    """java.nio.ByteBuffer.hashCode() of the bytes b (JDK loop; ECMessageVerbHandler.java:328)."""
+    b = np.ascontiguousarray(b, np.uint8)
+    return int(lib().oracle_java_bytebuffer_hashcode(_p(b) if b.size else None, b.size))
+
+
+def zero_fill(content, code_length: int) -> np.ndarray:
+    """ELECT's SSTable buffer: allocateDirect(codeLength).put(content).put(zeros)
+    (ECMessageVerbHandler.java:292-310, ECParityUpdateVerbHandler.java:643-663)."""
+    out = np.zeros(code_length, np.uint8)
+    content = np.asarray(content, np.uint8)
+    out[: content.size] = content
     return out

@@ -146,6 +146,29 @@ def test_no_device_fails_loudly():
         _lib.unaligned_vector_ok()
 
 
+def test_flow_entry_points_validate_before_device_work():
+    """encode_ex / encode_update_ex: argument errors and the no-op cases need no device."""
+    from elect_amd import _lib
+    from elect_amd.coder import RSCoder
+    c = RSCoder(4, 2)
+    d = [np.zeros(64, np.uint8) for _ in range(6)]
+    p = [np.zeros(64, np.uint8) for _ in range(2)]
+    ins = [a.ctypes.data for a in d]
+    outs = [a.ctypes.data for a in p]
+    with pytest.raises(_lib.ECInvalidArgument):  # target data index out of range
+        c.encode_update_ex_host(ins, 4, outs, 64, old_new_lengths=[64, 64])
+    with pytest.raises(_lib.ECInvalidArgument):  # fused hash needs 2 + m <= 10
+        RSCoder(4, 9).encode_update_ex_host(ins + [0] * 5, 0, outs + [0] * 7, 64, hashed=True)
+    # hashCode() of an empty buffer is 1 (no device work)
+    assert c.encode_ex_host(ins[:4], outs, 0, hashed=True) == [1, 1]
+    assert c.encode_update_ex_host(ins, 0, outs, 0, hashed=True) == [1, 1]
+    if not gpu_available():
+        with pytest.raises(_lib.ECDeviceError):
+            c.encode_ex_host(ins[:4], outs, 64, data_lengths=[64, 3, 0, 64], hashed=True)
+        with pytest.raises(_lib.ECDeviceError):
+            c.encode_update_ex_host(ins, 1, outs, 64, old_new_lengths=[10, 64], hashed=True)
+
+
 def test_partition_by_bytes():
     from elect_amd.batch import partition_by_bytes
     sizes = [1024] * 1000 + [4096] * 250 + [1 << 20] * 1

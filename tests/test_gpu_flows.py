@@ -1,0 +1,211 @@
+"""GPU parity of ELECT's two coding-node steps, each fused into one pass.
+
+- encode step, JEC/net/ECMessageVerbHandler.java:283-329: SSTable contents zero
+  filled to codeLength, encode, parity hashCode() (names the parity blocks);
+- parity-update step, JEC/net/ECParityUpdateVerbHandler.java:634-699: old and
+  new SSTable contents zero filled to codeLength, encodeUpdate, new-parity
+  hashCode().
+
+Expected values come from the oracle alone: zero fill (oracle.zero_fill), the
+L1 coder restatement (oracle.Encoder) and the JDK hashCode loop
+(oracle.java_hashcode).  Bar: bit-exact bytes and equal int32 hashes.  The
+buffers hold 0xFF garbage past every content length, which must not leak in.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _to(dev, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _garbage_past(a, lens):
+    """a[..., n:] = 0xFF past each length (last axis)."""
+    out = a.copy()
+    flat = out.reshape(-1, out.shape[-1])
+    for i, n in enumerate(np.asarray(lens).reshape(-1)):
+        flat[i, n:] = 0xFF
+    return out
+
+
+def _lengths(rng, B, n, L):
+    lens = rng.integers(0, L + 1, size=(B, n)).astype(np.int32)
+    lens[0, :] = L          # full units
+    if B > 1:
+        lens[1, :] = 0      # empty (ELECT's all-zero filler chunks)
+    if B > 2:
+        lens[2, :] = np.minimum(L, 16 * np.arange(1, n + 1) + 5)
+    return lens
+
+
+ENC_CASES = [(4, 2, 65536), (4, 2, 4099), (4, 2, 1), (4, 2, 1040), (8, 4, 2048), (3, 2, 4404020 // 64),
+             (10, 4, 333), (4, 6, 16008), (6, 3, 65536 + 16)]
+
+
+@pytest.mark.parametrize("k,m,L", ENC_CASES)
+@pytest.mark.parametrize("padded,hashed", [(True, True), (True, False), (False, True)])
+def test_encode_batch_ex(dev, oracle, k, m, L, padded, hashed):
+    from elect_amd.batch import encode_batch_ex
+    from elect_amd.coder import RSCoder
+    rng = np.random.default_rng(L + 7 * k + 3 * m)
+    B = 5
+    data = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    lens = _lengths(rng, B, k, L) if padded else np.full((B, k), L, np.int32)
+    par = torch.full((B, m, L), 0x5A, dtype=torch.uint8, device=dev)
+    hashes = torch.zeros((B, m), dtype=torch.int32, device=dev) if hashed else None
+    encode_batch_ex(RSCoder(k, m), _to(dev, _garbage_past(data, lens) if padded else data), par,
+                    lengths=_to(dev, lens) if padded else None, hashes=hashes)
+    got = par.cpu().numpy()
+    got_h = hashes.cpu().numpy() if hashed else None
+    enc = oracle.Encoder(k, m)
+    for s in range(B):
+        want = enc.encode([oracle.zero_fill(data[s, j, :lens[s, j]], L) for j in range(k)])
+        for r in range(m):
+            assert np.array_equal(got[s, r], want[r]), (s, r)
+            if hashed:
+                assert int(got_h[s, r]) == oracle.java_hashcode(want[r]), (s, r)
+
+
+UPD_CASES = [(4, 2, 65536), (4, 2, 4099), (4, 2, 17), (8, 4, 1024), (6, 6, 2048), (2, 8, 333), (4, 2, 1040)]
+
+
+@pytest.mark.parametrize("k,m,L", UPD_CASES)
+@pytest.mark.parametrize("padded,hashed", [(True, True), (True, False), (False, True)])
+@pytest.mark.parametrize("in_place", [False, True])
+def test_encode_update_batch_ex(dev, oracle, k, m, L, padded, hashed, in_place):
+    """m = 6, 8: two row groups, the second reading parity the first overwrote in place."""
+    from elect_amd.batch import encode_update_batch_ex
+    from elect_amd.coder import RSCoder
+    rng = np.random.default_rng(L * 5 + k + m)
+    B = 4
+    target = int(rng.integers(0, k))
+    old = rng.integers(0, 256, (B, L), dtype=np.uint8)
+    new = rng.integers(0, 256, (B, L), dtype=np.uint8)
+    pin = rng.integers(0, 256, (B, m, L), dtype=np.uint8)
+    lens = _lengths(rng, B, 2, L) if padded else np.full((B, 2), L, np.int32)
+    d_old = _to(dev, _garbage_past(old, lens[:, 0]) if padded else old)
+    d_new = _to(dev, _garbage_past(new, lens[:, 1]) if padded else new)
+    d_pin = _to(dev, pin)
+    d_pout = d_pin if in_place else torch.full((B, m, L), 0x77, dtype=torch.uint8, device=dev)
+    hashes = torch.zeros((B, m), dtype=torch.int32, device=dev) if hashed else None
+    encode_update_batch_ex(RSCoder(k, m), target, d_old, d_new, d_pin, d_pout,
+                           lengths=_to(dev, lens) if padded else None, hashes=hashes)
+    got = d_pout.cpu().numpy()
+    got_h = hashes.cpu().numpy() if hashed else None
+    enc = oracle.Encoder(k, m)
+    for s in range(B):
+        ins = [oracle.zero_fill(old[s, :lens[s, 0]], L), oracle.zero_fill(new[s, :lens[s, 1]], L)]
+        want = enc.encode_update(ins + [pin[s, r] for r in range(m)], target)
+        for r in range(m):
+            assert np.array_equal(got[s, r], want[r]), (s, r)
+            if hashed:
+                assert int(got_h[s, r]) == oracle.java_hashcode(want[r]), (s, r)
+
+
+def test_update_ex_hash_needs_m_le_8(dev):
+    from elect_amd import _lib
+    from elect_amd.batch import encode_update_batch_ex
+    from elect_amd.coder import RSCoder
+    B, L, m = 2, 64, 9
+    z = torch.zeros((B, L), dtype=torch.uint8, device=dev)
+    p = torch.zeros((B, m, L), dtype=torch.uint8, device=dev)
+    with pytest.raises(_lib.ECInvalidArgument):
+        encode_update_batch_ex(RSCoder(4, m), 0, z, z, p, p, hashes=torch.zeros((B, m), dtype=torch.int32,
+                                                                                  device=dev))
+    encode_update_batch_ex(RSCoder(4, m), 0, z, z, p, p, lengths=torch.zeros((B, 2), dtype=torch.int32,
+                                                                             device=dev))  # padded alone is fine
+
+
+def test_elect_flow_encode_then_update(dev, oracle):
+    """ELECT's lifecycle on one batch of stripes: transition (padded + hashed encode),
+    then compaction replaces SSTable `t` (padded + hashed update, in place).  The
+    updated parity and its hashes must equal a fresh encode of the new contents."""
+    from elect_amd.batch import encode_batch_ex, encode_update_batch_ex
+    from elect_amd.coder import RSCoder
+    k, m, B, L = 4, 2, 8, 65536 + 4  # codeLength = ceil(1.05 * size) is rarely a multiple of 16
+    rng = np.random.default_rng(77)
+    c = RSCoder(k, m)
+    data = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    lens = rng.integers(L // 2, L + 1, size=(B, k)).astype(np.int32)
+    d_data = _to(dev, _garbage_past(data, lens))
+    par = torch.empty((B, m, L), dtype=torch.uint8, device=dev)
+    h0 = torch.empty((B, m), dtype=torch.int32, device=dev)
+    encode_batch_ex(c, d_data, par, lengths=_to(dev, lens), hashes=h0)
+    t = 2
+    new = rng.integers(0, 256, (B, L), dtype=np.uint8)
+    new_lens = rng.integers(0, L + 1, size=B).astype(np.int32)
+    ul = np.stack([lens[:, t], new_lens], axis=1).astype(np.int32)
+    h1 = torch.empty((B, m), dtype=torch.int32, device=dev)
+    encode_update_batch_ex(c, t, d_data[:, t], _to(dev, _garbage_past(new, new_lens)), par, par,
+                           lengths=_to(dev, ul), hashes=h1)
+    lens2 = lens.copy()
+    lens2[:, t] = new_lens
+    data2 = data.copy()
+    data2[:, t] = new
+    ref = torch.empty_like(par)
+    h2 = torch.empty_like(h1)
+    encode_batch_ex(c, _to(dev, _garbage_past(data2, lens2)), ref, lengths=_to(dev, lens2), hashes=h2)
+    torch.cuda.synchronize()
+    assert torch.equal(par, ref)
+    assert torch.equal(h1, h2)
+    enc = oracle.Encoder(k, m)
+    want = enc.encode([oracle.zero_fill(data2[0, j, :lens2[0, j]], L) for j in range(k)])
+    assert int(h1[0, 1]) == oracle.java_hashcode(want[1])
+
+
+def test_host_encode_ex(dev, oracle):
+    """elect_ec_encode_ex: lengths across the 1 MiB pipeline step, NULL empty unit, hashes."""
+    from elect_amd.coder import RSCoder
+    k, m = 4, 2
+    L = (1 << 20) * 2 + 4404020 % 16 + 48
+    rng = np.random.default_rng(41)
+    lens = [L, (1 << 20) + 7, 0, 5]
+    bufs = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    addrs = [b.ctypes.data if n else None for b, n in zip(bufs, lens)]
+    par = [np.zeros(L, np.uint8) for _ in range(m)]
+    hs = RSCoder(k, m).encode_ex_host(addrs, [p.ctypes.data for p in par], L, data_lengths=lens, hashed=True)
+    want = oracle.Encoder(k, m).encode([oracle.zero_fill(b[:n], L) for b, n in zip(bufs, lens)])
+    for r in range(m):
+        assert np.array_equal(par[r], want[r])
+        assert hs[r] == oracle.java_hashcode(want[r])
+
+
+@pytest.mark.parametrize("L", [4404020, 4099, 1])
+@pytest.mark.parametrize("in_place", [False, True])
+def test_host_encode_update_ex(dev, oracle, L, in_place):
+    """elect_ec_encode_update_ex, as ECParityUpdateVerbHandler calls it: the old and
+    new SSTables shorter than codeLength, the new parity written over the old."""
+    from elect_amd.coder import RSCoder
+    k, m, t = 4, 2, 1
+    rng = np.random.default_rng(L + in_place)
+    old = rng.integers(0, 256, L, dtype=np.uint8)
+    new = rng.integers(0, 256, L, dtype=np.uint8)
+    pin = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(m)]
+    pin_copy = [p.copy() for p in pin]
+    lens = [max(0, L - 1000), L // 3]
+    out = pin if in_place else [np.zeros(L, np.uint8) for _ in range(m)]
+    hs = RSCoder(k, m).encode_update_ex_host([old.ctypes.data, new.ctypes.data] + [p.ctypes.data for p in pin], t,
+                                             [o.ctypes.data for o in out], L, old_new_lengths=lens, hashed=True)
+    want = oracle.Encoder(k, m).encode_update(
+        [oracle.zero_fill(old[:lens[0]], L), oracle.zero_fill(new[:lens[1]], L)] + pin_copy, t)
+    for r in range(m):
+        assert np.array_equal(out[r], want[r])
+        assert hs[r] == oracle.java_hashcode(want[r])
+
+
+def test_host_update_ex_empty_old(dev, oracle):
+    """A zero-length old SSTable may come as a NULL pointer."""
+    from elect_amd.coder import RSCoder
+    k, m, L, t = 4, 2, 5000, 3
+    rng = np.random.default_rng(3)
+    new = rng.integers(0, 256, L, dtype=np.uint8)
+    pin = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(m)]
+    out = [np.zeros(L, np.uint8) for _ in range(m)]
+    RSCoder(k, m).encode_update_ex_host([None, new.ctypes.data] + [p.ctypes.data for p in pin], t,
+                                        [o.ctypes.data for o in out], L, old_new_lengths=[0, L])
+    want = oracle.Encoder(k, m).encode_update([np.zeros(L, np.uint8), new] + pin, t)
+    for r in range(m):
+        assert np.array_equal(out[r], want[r])

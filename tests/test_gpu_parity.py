@@ -168,7 +168,7 @@ def test_unaligned_layouts(dev, oracle, shift, L):
     kernels run on unaligned addresses (rs_kernels.hip unaligned_vector_ok);
     encode, decode, update and the fused hash must stay bit-exact."""
     from elect_amd.batch import decode_batch, encode_batch, encode_batch_hashed, encode_update_batch
-    from elect_amd.coder import RSCoder, java_bytebuffer_hash
+    from elect_amd.coder import RSCoder
     k, m, B = 4, 2, 5
     rng = np.random.default_rng(shift * 1000 + L)
     c = RSCoder(k, m)
@@ -183,7 +183,7 @@ def test_unaligned_layouts(dev, oracle, shift, L):
     for s in range(B):
         for r in range(m):
             assert np.array_equal(got[s, r], want[s][r]), (s, r)
-            assert int(gh[s, r]) == java_bytebuffer_hash(want[s][r])
+            assert int(gh[s, r]) == oracle.java_hashcode(want[s][r])
     pv2 = _shifted(dev, np.zeros((B, m, L), np.uint8), (shift + 7) % 16)
     encode_batch(c, view, pv2)
     assert np.array_equal(pv2.cpu().numpy(), got)
@@ -406,7 +406,7 @@ def test_encode_batch_hashed_matches_java_hashcode(dev, oracle, k, m, L):
     (1040, 16008: every / some waves; the launch's last wave partial), the
     memset-and-add mode (< 64 segments per stripe) and row groups (m > 4)."""
     from elect_amd.batch import encode_batch_hashed
-    from elect_amd.coder import RSCoder, java_bytebuffer_hash
+    from elect_amd.coder import RSCoder
     rng = np.random.default_rng(L + 13 * k)
     B = 5
     data = _rand(rng, B, k, L)
@@ -419,11 +419,11 @@ def test_encode_batch_hashed_matches_java_hashcode(dev, oracle, k, m, L):
         want = enc.encode([data[s, j] for j in range(k)])
         for r in range(m):
             assert np.array_equal(got_p[s, r], want[r])
-            assert int(got_h[s, r]) == java_bytebuffer_hash(want[r]), (s, r)
+            assert int(got_h[s, r]) == oracle.java_hashcode(want[r]), (s, r)
 
 
 def test_encode_hashed_host_path(dev, oracle):
-    from elect_amd.coder import RSCoder, java_bytebuffer_hash
+    from elect_amd.coder import RSCoder
     k, m = 4, 2
     for L in (4404020, 17, 0):
         rng = np.random.default_rng(L)
@@ -433,7 +433,7 @@ def test_encode_hashed_host_path(dev, oracle):
         want = oracle.Encoder(k, m).encode(d) if L else [np.zeros(0, np.uint8)] * m
         for r in range(m):
             assert np.array_equal(p[r], want[r])
-            assert hs[r] == java_bytebuffer_hash(want[r])
+            assert hs[r] == oracle.java_hashcode(want[r])
 
 
 def test_host_device_policy(dev, oracle):

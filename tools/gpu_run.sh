@@ -67,6 +67,9 @@ for step in "$@"; do
     hashed)
         run bench_hashed 400 python bench.py --config hashed || exit $?
         run bench_hashed_1M 400 python bench.py --config hashed --chunk 1048576 || exit $? ;;
+    flows)  # ELECT's two coding-node steps, fused (padded + hashed encode, padded + hashed update)
+        run bench_flows 400 python bench.py --config flows || exit $?
+        run bench_flows_elect 400 python bench.py --config flows --chunk 4404020 --stripes 256 || exit $? ;;
     hostsweep) run hostsweep 600 python tools/tune/host_sweep.py || exit $? ;;
     copysizes) run copysizes 600 python tools/tune/host_sweep.py copysizes || exit $? ;;
     staged)
