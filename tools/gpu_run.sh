@@ -92,8 +92,11 @@ for step in "$@"; do
         for i in 1 2 3; do for v in a ${AB_VARIANTS:-b}; do
             lib=""; [ $v = a ] || lib="$PWD/elect_amd/_ab/libelect_ec_$v.so"
             for c in ${AB_CONFIGS:-headline rs12 padded}; do
-                cfg=${c%%:*}; extra=""; [ "$cfg" != "$c" ] && extra="--pad-fill ${c#*:}"
-                ELECT_EC_LIB=$lib run "ab_${v}_${c/:/-}_$i" 300 python bench.py --config $cfg $extra --no-cpu --no-host --steps 50 || exit $?
+                # cfg[:padfill][+arg+arg...]: e.g. padded:0.5, flows+--chunk+4404020+--stripes+256
+                base=${c%%+*}; args=""; [ "$base" != "$c" ] && args="${c#*+}" && args="${args//+/ }"
+                cfg=${base%%:*}; extra=""; [ "$cfg" != "$base" ] && extra="--pad-fill ${base#*:}"
+                tag=${c//[:+]/-}; tag=${tag//--/}
+                ELECT_EC_LIB=$lib run "ab_${v}_${tag}_$i" 300 python bench.py --config $cfg $extra $args --no-cpu --no-host --steps 50 || exit $?
             done
         done; done ;;
     padfill)  # padded encode vs content fill: where the time goes
