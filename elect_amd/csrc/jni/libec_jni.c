@@ -1,13 +1,15 @@
 /*
  * libec_jni.c — drop-in replacement for ELECT's JNI library libec.so.
  *
- * Exports exactly the seven native methods ELECT's Java binds
+ * Exports the seven native methods ELECT's Java binds
  * (JEC/NativeRSEncoder.java:97-105, JEC/NativeRSDecoder.java:81-87; the
  * reference implementations are EC/NativeRSEncoder.c:31-95 and
  * EC/NativeRSDecoder.c:32-82) and forwards them to the MI355X C ABI
  * (include/elect_ec.h).  Built only where a JDK provides <jni.h>; see
  * INTEGRATION.md for the build line.  No Java code changes: ELECT keeps calling
- * System.loadLibrary("ec") (JEC/NativeRSEncoder.java:37).
+ * System.loadLibrary("ec") (JEC/NativeRSEncoder.java:37).  Two optional
+ * methods (encodeExImpl, encodeUpdateExImpl) expose the fused coding-node
+ * steps to a Java that declares them.
  *
  * Differences from the reference glue, all on error paths:
  *  - every THROW returns (EC/NativeRSDecoder.c:50-52 and EC/jni_common.c:70-73,
@@ -178,6 +180,103 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeUpdateImpl(JNIEnv
                  elect_ec_encode_update(c, (const unsigned char* const*)in, targetUpdateDataIndex, out,
                                         (size_t)dataLen),
                  "encodeUpdate");
+}
+
+/* ---- optional: ELECT's coding-node steps fused (not bound by the unchanged Java) ----
+ * A maintainer who adds the matching `private native` methods to NativeRSEncoder
+ *  gets ECMessageVerbHandler's zero fill + encode + parity
+ * hashCode (:283-329) and ECParityUpdateVerbHandler's zero fill + encodeUpdate +
+ * new-parity hashCode (:634-699) in one call each.  contentLengths (k entries for
+ * encode, 2 for [old, new]) and parityHashes (>= m entries, written) may be null. */
+static int content_lengths(JNIEnv* env, jintArray arr, int n, size_t* out, const size_t** use)
+{
+    *use = NULL;
+    if (arr == NULL)
+        return 0;
+    jint v[EC_MAX];
+    if ((*env)->GetArrayLength(env, arr) != n || n > EC_MAX) {
+        throw_java(env, "java/lang/InternalError", "Invalid content lengths");
+        return 1;
+    }
+    (*env)->GetIntArrayRegion(env, arr, 0, n, v);
+    for (int i = 0; i < n; i++) {
+        if (v[i] < 0) {
+            throw_java(env, "java/lang/IllegalArgumentException", "negative content length");
+            return 1;
+        }
+        out[i] = (size_t)v[i];
+    }
+    *use = out;
+    return 0;
+}
+
+static int hash_array(JNIEnv* env, jintArray arr, int m)
+{
+    if (arr != NULL && (*env)->GetArrayLength(env, arr) < m) {
+        throw_java(env, "java/lang/InternalError", "Invalid parity hashes");
+        return 1;
+    }
+    return 0;
+}
+
+JNIEXPORT void JNICALL
+Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeExImpl(JNIEnv* env, jobject thiz,
+                                                                      jobjectArray inputs, jintArray inputOffsets,
+                                                                      jintArray contentLengths, jint dataLen,
+                                                                      jobjectArray outputs, jintArray outputOffsets,
+                                                                      jintArray parityHashes)
+{
+    unsigned char* in[2 + EC_MAX];
+    unsigned char* out[2 + EC_MAX];
+    size_t lens[EC_MAX];
+    const size_t* use_lens;
+    jint h[EC_MAX];
+    elect_ec_coder* c = get_coder(env, thiz);
+    if (c == NULL) {
+        throw_java(env, "java/io/IOException", "NativeRSRawEncoder closed");
+        return;
+    }
+    int k = elect_ec_coder_num_data_units(c), m = elect_ec_coder_num_parity_units(c);
+    if (buffers(env, inputs, inputOffsets, k, in, "Invalid inputs") ||
+        buffers(env, outputs, outputOffsets, m, out, "Invalid outputs") ||
+        content_lengths(env, contentLengths, k, lens, &use_lens) || hash_array(env, parityHashes, m))
+        return;
+    if (raise_status(env,
+                     elect_ec_encode_ex(c, (const unsigned char* const*)in, use_lens, out, (size_t)dataLen,
+                                        parityHashes ? (int32_t*)h : NULL),
+                     "encodeEx"))
+        return;
+    if (parityHashes != NULL)
+        (*env)->SetIntArrayRegion(env, parityHashes, 0, m, h);
+}
+
+JNIEXPORT void JNICALL
+Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeUpdateExImpl(
+    JNIEnv* env, jobject thiz, jobjectArray inputs, jintArray inputOffsets, jintArray contentLengths, jint dataLen,
+    jint targetUpdateDataIndex, jobjectArray outputs, jintArray outputOffsets, jintArray parityHashes)
+{
+    unsigned char* in[2 + EC_MAX];
+    unsigned char* out[2 + EC_MAX];
+    size_t lens[EC_MAX];
+    const size_t* use_lens;
+    jint h[EC_MAX];
+    elect_ec_coder* c = get_coder(env, thiz);
+    if (c == NULL) {
+        throw_java(env, "java/io/IOException", "NativeRSRawEncoder closed");
+        return;
+    }
+    int m = elect_ec_coder_num_parity_units(c);
+    if (buffers(env, inputs, inputOffsets, 2 + m, in, "Invalid inputs") ||
+        buffers(env, outputs, outputOffsets, m, out, "Invalid outputs") ||
+        content_lengths(env, contentLengths, 2, lens, &use_lens) || hash_array(env, parityHashes, m))
+        return;
+    if (raise_status(env,
+                     elect_ec_encode_update_ex(c, (const unsigned char* const*)in, use_lens, targetUpdateDataIndex,
+                                               out, (size_t)dataLen, parityHashes ? (int32_t*)h : NULL),
+                     "encodeUpdateEx"))
+        return;
+    if (parityHashes != NULL)
+        (*env)->SetIntArrayRegion(env, parityHashes, 0, m, h);
 }
 
 JNIEXPORT void JNICALL

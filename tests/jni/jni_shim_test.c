@@ -206,6 +206,17 @@ static void m_GetIntArrayRegion(JNIEnv* env, jintArray a, jsize start, jsize len
     memcpy(buf, a->ints + start, sizeof(jint) * len);
 }
 
+static void m_SetIntArrayRegion(JNIEnv* env, jintArray a, jsize start, jsize len, const jint* buf)
+{
+    (void)env;
+    no_pending("SetIntArrayRegion");
+    if (start < 0 || len < 0 || start + len > a->n) {
+        raise_exc("java/lang/ArrayIndexOutOfBoundsException", "");
+        return;
+    }
+    memcpy(a->ints + start, buf, sizeof(jint) * len);
+}
+
 static void* m_GetDirectBufferAddress(JNIEnv* env, jobject o)
 {
     (void)env;
@@ -223,7 +234,8 @@ static const struct JNINativeInterface_ kEnvTable = {
     m_FindClass,         m_ThrowNew,           m_ExceptionClear,        m_GetObjectClass,
     m_GetFieldID,        m_GetMethodID,        m_CallBooleanMethod,     m_GetLongField,
     m_SetLongField,      m_GetArrayLength,     m_GetObjectArrayElement, m_GetIntArrayElements,
-    m_ReleaseIntArrayElements, m_GetIntArrayRegion, m_GetDirectBufferAddress, m_DeleteLocalRef,
+    m_ReleaseIntArrayElements, m_GetIntArrayRegion, m_SetIntArrayRegion, m_GetDirectBufferAddress,
+    m_DeleteLocalRef,
 };
 static JNIEnv kEnv = &kEnvTable;
 static JNIEnv* env = &kEnv;
@@ -233,6 +245,11 @@ typedef void (*init_fn)(JNIEnv*, jobject, jint, jint);
 typedef void (*encode_fn)(JNIEnv*, jobject, jobjectArray, jintArray, jint, jobjectArray, jintArray);
 typedef void (*update_fn)(JNIEnv*, jobject, jobjectArray, jintArray, jint, jint, jobjectArray, jintArray);
 typedef void (*destroy_fn)(JNIEnv*, jobject);
+/* optional fused methods: (inputs, offsets, contentLengths, dataLen[, target], outputs, offsets, hashes) */
+typedef void (*encode_ex_fn)(JNIEnv*, jobject, jobjectArray, jintArray, jintArray, jint, jobjectArray, jintArray,
+                             jintArray);
+typedef void (*update_ex_fn)(JNIEnv*, jobject, jobjectArray, jintArray, jintArray, jint, jint, jobjectArray,
+                             jintArray, jintArray);
 typedef void (*decode_fn)(JNIEnv*, jobject, jobjectArray, jintArray, jint, jintArray, jintArray, jobjectArray,
                           jintArray);
 
@@ -242,6 +259,8 @@ static struct {
     update_fn update;
     decode_fn decode;
     destroy_fn enc_destroy, dec_destroy;
+    encode_ex_fn encode_ex;
+    update_ex_fn update_ex;
     int (*device_count)(int*);
 } jni;
 
@@ -270,6 +289,8 @@ static void load(const char* lib)
     jni.dec_init = (init_fn)sym(h, PFX "NativeRSDecoder_initImpl");
     jni.decode = (decode_fn)sym(h, PFX "NativeRSDecoder_decodeImpl");
     jni.dec_destroy = (destroy_fn)sym(h, PFX "NativeRSDecoder_destroyImpl");
+    jni.encode_ex = (encode_ex_fn)sym(h, PFX "NativeRSEncoder_encodeExImpl");
+    jni.update_ex = (update_ex_fn)sym(h, PFX "NativeRSEncoder_encodeUpdateExImpl");
     jni.device_count = (int (*)(int*))sym(h, "elect_ec_device_count");
 }
 
@@ -387,6 +408,29 @@ static int cpu_checks(void)
         EXPECT(threw("java/io/IOException", "no HIP device"));
     }
 
+    /* optional fused methods: argument checks */
+    const jint cl4[4] = {16, 3, 0, 16}, cl3[3] = {16, 16, 16}, cl_neg[4] = {16, -1, 0, 16}, cl2[2] = {5, 16};
+    jobject hashes2 = int_array(2, cl2), hashes1 = int_array(1, cl2);
+    jni.encode_ex(env, enc, in4, off4, int_array(3, cl3), 16, out2, poff2, hashes2);
+    EXPECT(threw("java/lang/InternalError", "Invalid content lengths"));
+    jni.encode_ex(env, enc, in4, off4, int_array(4, cl_neg), 16, out2, poff2, NULL);
+    EXPECT(threw("java/lang/IllegalArgumentException", "negative content length"));
+    jni.encode_ex(env, enc, in4, off4, int_array(4, cl4), 16, out2, poff2, hashes1);
+    EXPECT(threw("java/lang/InternalError", "Invalid parity hashes"));
+    jni.encode_ex(env, enc, in4, off4, int_array(4, cl4), 0, out2, poff2, hashes2);  /* empty: hashCode 1 */
+    EXPECT(clean());
+    EXPECT(hashes2->ints[0] == 1 && hashes2->ints[1] == 1);
+    jni.update_ex(env, enc, in4, off4, int_array(4, cl4), 16, 0, out2, poff2, NULL);
+    EXPECT(threw("java/lang/InternalError", "Invalid content lengths"));
+    jni.update_ex(env, enc, in4, off4, int_array(2, cl2), 16, 9, out2, poff2, NULL);  /* target >= k */
+    EXPECT(threw("java/lang/IllegalArgumentException", "invalid argument"));
+    if (ndev == 0) {
+        jni.encode_ex(env, enc, in4, off4, int_array(4, cl4), 16, out2, poff2, hashes2);
+        EXPECT(threw("java/io/IOException", "no HIP device"));
+        jni.update_ex(env, enc, in4, off4, int_array(2, cl2), 16, 1, out2, poff2, hashes2);
+        EXPECT(threw("java/io/IOException", "no HIP device"));
+    }
+
     /* destroy zeroes the field; use after destroy -> IOException (EC/NativeRSEncoder.c:46-50) */
     jni.enc_destroy(env, enc);
     EXPECT(clean());
@@ -396,6 +440,10 @@ static int cpu_checks(void)
     jni.encode(env, enc, in4, off4, 16, out2, poff2);
     EXPECT(threw("java/io/IOException", "NativeRSRawEncoder closed"));
     jni.update(env, enc, in4, off4, 16, 0, out2, poff2);
+    EXPECT(threw("java/io/IOException", "NativeRSRawEncoder closed"));
+    jni.encode_ex(env, enc, in4, off4, NULL, 16, out2, poff2, NULL);
+    EXPECT(threw("java/io/IOException", "NativeRSRawEncoder closed"));
+    jni.update_ex(env, enc, in4, off4, NULL, 16, 0, out2, poff2, NULL);
     EXPECT(threw("java/io/IOException", "NativeRSRawEncoder closed"));
 
     /* decoder */
@@ -531,6 +579,75 @@ static int gpu_erasure_code_test(const char* outdir)
     return failures;
 }
 
+/* JDK ByteBuffer.hashCode() loop over [p, p+n) */
+static jint java_hash(const unsigned char* p, size_t n)
+{
+    uint32_t h = 1;
+    for (size_t i = n; i-- > 0;) h = 31u * h + (uint32_t)(int32_t)(signed char)p[i];
+    return (jint)h;
+}
+
+/* The optional fused methods against the seven plain ones: encodeEx over
+ * SSTable contents shorter than codeLength (0xEE garbage past each) equals
+ * encode over the zero-filled buffers, with the JDK hashCode of each parity;
+ * encodeUpdateEx (new parity over the old, in place) equals encoding the
+ * zero-filled new stripe. */
+static int gpu_fused_flows(void)
+{
+    enum { K = 4, M = 2 };
+    const jint L = 70001;
+    JavaRandom rnd;
+    jr_init(&rnd, 321);
+    struct Bufs raw, filled, par, ref, newd, ref2;
+    bufs_init(&raw, K, L, 1);
+    bufs_init(&filled, K, L, 2);
+    bufs_init(&par, M, L, 3);
+    bufs_init(&ref, M, L, 4);
+    bufs_init(&newd, 1, L, 5);
+    bufs_init(&ref2, M, L, 6);
+    const jint lens[K] = {L, L - 4099, 0, 17};
+    for (int i = 0; i < K; ++i) {
+        jr_next_bytes(&rnd, at(&raw, i), L);
+        memcpy(at(&filled, i), at(&raw, i), lens[i]);  /* calloc'd: zero past the content */
+        memset(at(&raw, i) + lens[i], 0xEE, L - lens[i]);
+    }
+    jobject enc = coder_obj(ENC_CLS);
+    jni.enc_init(env, enc, K, M);
+    jobject hashes = int_array(M, lens);
+    jni.encode_ex(env, enc, obj_array(K, raw.bb), int_array(K, raw.pos), int_array(K, lens), L,
+                  obj_array(M, par.bb), int_array(M, par.pos), hashes);
+    EXPECT(clean());
+    jni.encode(env, enc, obj_array(K, filled.bb), int_array(K, filled.pos), L, obj_array(M, ref.bb),
+               int_array(M, ref.pos));
+    EXPECT(clean());
+    for (int r = 0; r < M; ++r) {
+        EXPECT(!memcmp(at(&par, r), at(&ref, r), L));
+        EXPECT(hashes->ints[r] == java_hash(at(&ref, r), L));
+    }
+    /* compaction replaces unit 1: old content lens[1] bytes, new content 5000 bytes */
+    const jint ulens[2] = {lens[1], 5000};
+    jr_next_bytes(&rnd, at(&newd, 0), L);
+    jobject uin[2 + M] = {raw.bb[1], newd.bb[0], par.bb[0], par.bb[1]};
+    jint uin_pos[2 + M] = {raw.pos[1], newd.pos[0], par.pos[0], par.pos[1]};
+    jni.update_ex(env, enc, obj_array(2 + M, uin), int_array(2 + M, uin_pos), int_array(2, ulens), L, 1,
+                  obj_array(M, par.bb), int_array(M, par.pos), hashes);
+    EXPECT(clean());
+    memset(at(&filled, 1), 0, L);
+    memcpy(at(&filled, 1), at(&newd, 0), ulens[1]);
+    jni.encode(env, enc, obj_array(K, filled.bb), int_array(K, filled.pos), L, obj_array(M, ref2.bb),
+               int_array(M, ref2.pos));
+    EXPECT(clean());
+    for (int r = 0; r < M; ++r) {
+        EXPECT(!memcmp(at(&par, r), at(&ref2, r), L));
+        EXPECT(hashes->ints[r] == java_hash(at(&ref2, r), L));
+    }
+    jni.enc_destroy(env, enc);
+    EXPECT(vm.violations == 0);
+    EXPECT(vm.live_int_elems == 0);
+    EXPECT(vm.local_refs == 0);
+    return failures;
+}
+
 int main(int argc, char** argv)
 {
     if (argc < 3) {
@@ -539,7 +656,8 @@ int main(int argc, char** argv)
     }
     load(argv[1]);
     const int gpu = !strcmp(argv[2], "gpu");
-    const int rc = gpu ? gpu_erasure_code_test(argc > 3 ? argv[3] : ".") : cpu_checks();
+    int rc = gpu ? gpu_erasure_code_test(argc > 3 ? argv[3] : ".") : cpu_checks();
+    if (gpu && rc == 0) rc = gpu_fused_flows();
     printf("%s: %d failure(s), %d JNI violation(s)\n", argv[2], rc, vm.violations);
     return rc == 0 ? 0 : 1;
 }

@@ -55,6 +55,7 @@ struct JNINativeInterface_ {
     jint* (*GetIntArrayElements)(JNIEnv*, jintArray, jboolean*);
     void (*ReleaseIntArrayElements)(JNIEnv*, jintArray, jint*, jint);
     void (*GetIntArrayRegion)(JNIEnv*, jintArray, jsize, jsize, jint*);
+    void (*SetIntArrayRegion)(JNIEnv*, jintArray, jsize, jsize, const jint*);
     void* (*GetDirectBufferAddress)(JNIEnv*, jobject);
     void (*DeleteLocalRef)(JNIEnv*, jobject);
 };
