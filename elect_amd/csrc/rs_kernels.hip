@@ -662,6 +662,9 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         bool lens_path = false;
         if constexpr (PAD) {
             lens_path = a.lens && !a.hashes && p.aligned16 && p.len % 16 == 0 && p.len < (uint64_t{1} << 31);
+#ifdef AB_NO_LENS
+            lens_path = false;
+#endif
             if (lens_path) {
                 constexpr int U = lens_unroll<K>();
                 const uint64_t threads = (static_cast<uint64_t>(a.total) + 64 * U - 1) / (64 * U) * 64;
