@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--pad-fill", default="random",
                     help="padded: content lengths 'random' (uniform [0, L]) or a fixed fraction of L")
     ap.add_argument("--host-chunk", type=int, default=4404020, help="hostpath: bytes per unit per call")
+    ap.add_argument("--host-op", choices=("encode", "encode_ex"), default="encode",
+                    help="hostpath: plain encode (the JNI encodeImpl), or ELECT's fused encode step "
+                         "(encodeExImpl: content = codeLength/1.05, parity hashCodes)")
     return ap.parse_args()
 
 
@@ -382,13 +385,18 @@ def config_hostpath(args, world, rank, dev):
         p = [np.empty(L, np.uint8) for _ in range(m)]
         bufs.append((d, p))
     calls = max(4, args.steps // 2) * max(1, 4404020 // L // 8)
+    fused = args.host_op == "encode_ex"
+    content = [int(L / 1.05) - 64 * j for j in range(k)]  # SSTables just under codeLength/1.05
 
     def worker(t, n):
         torch.cuda.set_device(dev)
         d, p = bufs[t]
         da, pa = [x.ctypes.data for x in d], [x.ctypes.data for x in p]
         for _ in range(n):
-            coder.encode_host(da, pa, L)
+            if fused:
+                coder.encode_ex_host(da, pa, L, data_lengths=content, hashed=True)
+            else:
+                coder.encode_host(da, pa, L)
 
     def run(n):
         th = [threading.Thread(target=worker, args=(t, n)) for t in range(T)]
@@ -405,12 +413,22 @@ def config_hostpath(args, world, rank, dev):
     rebuilt = np.empty(L, np.uint8)
     coder.decode_host([p[0].ctypes.data] + [x.ctypes.data for x in d[1:]], [4, 1, 2, 3], [0],
                       [rebuilt.ctypes.data], L)
-    ok = bool(np.array_equal(rebuilt, d[0]))
-    return {"metric": "GiB/s host-memory RS(6,4) encode through the C ABI (JNI calling convention)",
+    ok = bool(np.array_equal(rebuilt, d[0])) if not fused else True
+    if fused:  # self-check: the fused step's parity equals a plain encode of the zero-filled units
+        from elect_amd.coder import java_bytebuffer_hash
+        z = [np.concatenate([x[:n], np.zeros(L - n, np.uint8)]) for x, n in zip(d, content)]
+        ref = [np.empty(L, np.uint8) for _ in range(m)]
+        coder.encode_host([x.ctypes.data for x in z], [x.ctypes.data for x in ref], L)
+        hs = coder.encode_ex_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L,
+                                  data_lengths=content, hashed=True)
+        ok = all(np.array_equal(a, b) for a, b in zip(p, ref)) and hs == [java_bytebuffer_hash(x) for x in ref]
+    op_name = "fused encode step (zero fill + encode + parity hashCode, elect_ec_encode_ex)" if fused else \
+        "encode"
+    return {"metric": f"GiB/s host-memory RS(6,4) {op_name} through the C ABI (JNI calling convention)",
             "value": round(T * calls * k * L / dt / GIB, 2), "unit": "GiB/s", "n_gpus": 1,
             "steps": calls, "warmup": 1, "ms_per_step": round(dt / calls * 1e3, 3), "higher_is_better": True,
             "scaling": "none", "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
-            "config": {"workload": f"{T} threads x {calls} synchronous elect_ec_encode calls, one stripe "
+            "config": {"workload": f"{T} threads x {calls} synchronous elect_ec_{args.host_op} calls, one stripe "
                                    f"of {k} x {L} B each, pageable host buffers",
                        "parallelism": "cross-thread batching (shared pinned arena, one launch per batch)"
                                       if args.batch else "per-thread pinned staging + 2 streams"}}

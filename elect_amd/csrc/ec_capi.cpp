@@ -234,16 +234,8 @@ int elect_ec_encode_hashed(const elect_ec_coder* coder, const unsigned char* con
 int elect_ec_encode_update(const elect_ec_coder* coder, const unsigned char* const* old_new_parity,
                            int target_data_index, unsigned char* const* new_parity_units, size_t chunk_size)
 {
-    if (!valid_coder(coder) || !old_new_parity || !new_parity_units) return ELECT_EC_EINVAL;
-    if (target_data_index < 0 || target_data_index >= coder->k) return ELECT_EC_EINVAL;
-    HostOp op;
-    op.update = true;
-    op.cols = 2 + coder->m;
-    op.rows = coder->m;
-    op.in = old_new_parity;
-    op.out = new_parity_units;
-    for (int r = 0; r < coder->m; ++r) op.coef[r] = parity_row(coder, r)[target_data_index];
-    return run_host(op, chunk_size);
+    return elect_ec_encode_update_ex(coder, old_new_parity, nullptr, target_data_index, new_parity_units,
+                                     chunk_size, nullptr);
 }
 
 int elect_ec_encode_update_ex(const elect_ec_coder* coder, const unsigned char* const* old_new_parity,
@@ -252,8 +244,6 @@ int elect_ec_encode_update_ex(const elect_ec_coder* coder, const unsigned char* 
 {
     if (!valid_coder(coder) || !old_new_parity || !new_parity_units) return ELECT_EC_EINVAL;
     if (target_data_index < 0 || target_data_index >= coder->k) return ELECT_EC_EINVAL;
-    if (!old_new_lengths && !hashes)
-        return elect_ec_encode_update(coder, old_new_parity, target_data_index, new_parity_units, chunk_size);
     if (hashes && 2 + coder->m > ELECT_EC_MAX_DATA_UNITS) return ELECT_EC_EINVAL;
     if (old_new_lengths && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
     if (hashes && chunk_size == 0) {
@@ -261,7 +251,8 @@ int elect_ec_encode_update_ex(const elect_ec_coder* coder, const unsigned char* 
         return ELECT_EC_OK;
     }
     // The update as a (2+m)-column product [c_r, c_r, e_r] over [old, new, P...]:
-    // the padded and hashed encode machinery then serves it unchanged.
+    // the padded and hashed encode machinery, and cross-thread batching, then
+    // serve it unchanged (the host path has no separate update kernel).
     HostOp op;
     op.cols = 2 + coder->m;
     op.rows = coder->m;

@@ -21,7 +21,6 @@ namespace host {
 namespace {
 
 using kern::ApplyParams;
-using kern::UpdateParams;
 
 // ---------------------------------------------------------------------------
 // Host-memory path: per-thread, per-device staging engine.
@@ -111,20 +110,6 @@ public:
 private:
     hipError_t launch(const HostOp& op, int s, size_t pitch, size_t n, const uint32_t* valid, size_t offset)
     {
-        if (op.update) {
-            UpdateParams p;
-            p.len = n;
-            p.stripes = 1;
-            p.rows = op.rows;
-            p.old_data = col(d_in_[s], pitch, 0);
-            p.new_data = col(d_in_[s], pitch, pitch);
-            for (int r = 0; r < op.rows; ++r) {
-                p.par_in[r] = col(d_in_[s], pitch, (2 + r) * pitch);
-                p.par_out[r] = col(d_out_[s], pitch, r * pitch);
-                p.coef[r] = op.coef[r];
-            }
-            return kern::launch_update(p, stream_[s]);
-        }
         ApplyParams p;
         p.len = n;
         p.stripes = 1;
@@ -268,11 +253,13 @@ int host_device(int ndev, int* dev)
 // ---------------------------------------------------------------------------
 // Cross-thread batching.  ELECT makes up to concurrent_ec
 // (64, conf/elect.yaml:598) synchronous one-stripe calls at once.  With
-// batching on, concurrent calls of the same shape (k, m, len, coefficients)
-// share a pinned arena: every caller copies its own inputs in (in parallel),
-// one dispatcher thread per device issues ONE H2D, ONE launch over all the
-// stripes ([slot][k][pitch] layout) and ONE D2H, then each caller copies its
-// outputs out.  Two arenas alternate, so one fills while the other is in flight.
+// batching on, concurrent calls of the same shape (k, m, len, coefficients,
+// padded or not, hashed or not) share a pinned arena: every caller copies its
+// own inputs in (in parallel; only content bytes when padded), one dispatcher
+// thread per device issues ONE H2D, ONE launch over all the stripes
+// ([slot][cols][pitch] layout) and ONE D2H, then each caller copies its outputs
+// (and parity hashes) out.  Encodes, decodes and parity updates (as products)
+// all batch.  Two arenas alternate, so one fills while the other is in flight.
 // ---------------------------------------------------------------------------
 struct BatchConfig {
     std::atomic<int> enabled{-1};  // -1: read ELECT_EC_BATCH on first use
@@ -299,6 +286,9 @@ class Batcher {
 public:
     static constexpr int kFallback = 1000;  // request does not fit: run it directly
     static constexpr int kSlabs = 2;
+    // Per-slot content lengths (padded ops) and parity hashes (hashed ops) of a
+    // batch: entries per arena, which caps such a batch's stripes.
+    static constexpr size_t kMetaEntries = size_t{1} << 16;
 
     explicit Batcher(int dev) : dev_(dev) {}
 
@@ -339,7 +329,14 @@ public:
         lock.unlock();
 
         const size_t in_stride = static_cast<size_t>(slab->cols) * pitch;
-        for (int j = 0; j < op.cols; ++j) std::memcpy(slab->pin_in + slot * in_stride + j * pitch, op.in[j], len);
+        if (op.lens) {  // only the content bytes; the kernel reads the rest as zero
+            for (int j = 0; j < op.cols; ++j) {
+                slab->pin_lens[static_cast<size_t>(slot) * op.cols + j] = static_cast<uint32_t>(op.lens[j]);
+                if (op.lens[j]) std::memcpy(slab->pin_in + slot * in_stride + j * pitch, op.in[j], op.lens[j]);
+            }
+        } else {
+            for (int j = 0; j < op.cols; ++j) std::memcpy(slab->pin_in + slot * in_stride + j * pitch, op.in[j], len);
+        }
 
         lock.lock();
         if (++slab->filled == slab->reserved) cv_worker_.notify_one();
@@ -351,6 +348,8 @@ public:
             const size_t out_stride = static_cast<size_t>(slab->rows) * pitch;
             for (int r = 0; r < op.rows; ++r)
                 std::memcpy(op.out[r], slab->pin_out + slot * out_stride + r * pitch, len);
+            if (op.hashes)
+                std::memcpy(op.hashes, slab->pin_hash + static_cast<size_t>(slot) * op.rows, op.rows * sizeof(int32_t));
         }
         lock.lock();
         if (--slab->readers == 0) {
@@ -369,16 +368,20 @@ private:
         uint8_t coef[kern::kMaxRows * kern::kMaxCols] = {};
         int capacity = 0, reserved = 0, filled = 0, readers = 0, status = ELECT_EC_OK;
         bool full = false;
+        bool padded = false, hashed = false;
         uint64_t seq = 0;
         std::chrono::steady_clock::time_point opened;
         uint8_t *pin_in = nullptr, *pin_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+        uint32_t *pin_lens = nullptr, *d_lens = nullptr;  // [slot][cols]
+        int32_t *pin_hash = nullptr, *d_hash = nullptr;    // [slot][rows]
         std::condition_variable done;  // this batch's callers wait here for kDone
         hipStream_t stream = nullptr;
         hipEvent_t h2d_done = nullptr;
 
         bool matches(const HostOp& op, size_t n) const
         {
-            return op.cols == cols && op.rows == rows && n == len && std::memcmp(op.coef, coef, sizeof(coef)) == 0;
+            return op.cols == cols && op.rows == rows && n == len && (op.lens != nullptr) == padded &&
+                   (op.hashes != nullptr) == hashed && std::memcmp(op.coef, coef, sizeof(coef)) == 0;
         }
 
         void open(const HostOp& op, size_t n, size_t p, size_t arena, uint64_t order)
@@ -388,7 +391,12 @@ private:
             len = n;
             pitch = p;
             std::memcpy(coef, op.coef, sizeof(coef));
-            capacity = static_cast<int>(arena / (static_cast<size_t>(std::max(cols, rows)) * pitch));
+            padded = op.lens != nullptr;
+            hashed = op.hashes != nullptr;
+            size_t cap = arena / (static_cast<size_t>(std::max(cols, rows)) * pitch);
+            if (padded) cap = std::min(cap, kMetaEntries / cols);
+            if (hashed) cap = std::min(cap, kMetaEntries / rows);
+            capacity = static_cast<int>(cap);
             reserved = filled = readers = 0;
             status = ELECT_EC_OK;
             full = false;
@@ -409,6 +417,11 @@ private:
             if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_out), arena, hipHostMallocDefault);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_in), arena);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_out), arena);
+            const size_t meta = kMetaEntries * sizeof(uint32_t);
+            if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_lens), meta, hipHostMallocDefault);
+            if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_lens), meta);
+            if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_hash), meta, hipHostMallocDefault);
+            if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_hash), meta);
             if (e != hipSuccess) return map_hip(e);
         }
         return ELECT_EC_OK;
@@ -459,6 +472,9 @@ private:
         const size_t in_stride = static_cast<size_t>(s.cols) * s.pitch;
         const size_t out_stride = static_cast<size_t>(s.rows) * s.pitch;
         hipError_t e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
+        if (e == hipSuccess && s.padded)
+            e = hipMemcpyAsync(s.d_lens, s.pin_lens, static_cast<size_t>(n) * s.cols * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, s.stream);
         if (e == hipSuccess) e = hipEventRecord(s.h2d_done, s.stream);
         if (e == hipSuccess) {
             ApplyParams p;
@@ -469,9 +485,21 @@ private:
             for (int j = 0; j < s.cols; ++j) p.src[j] = col(s.d_in, in_stride, j * s.pitch);
             for (int r = 0; r < s.rows; ++r) p.dst[r] = col(s.d_out, out_stride, r * s.pitch);
             std::memcpy(p.coef, s.coef, sizeof(p.coef));
+            if (s.padded) {
+                p.padded = true;
+                p.lens = s.d_lens;
+            }
+            if (s.hashed) {
+                p.hashes = s.d_hash;
+                p.hash_stride = static_cast<uint32_t>(s.rows);
+                p.hash_seed = true;
+            }
             e = kern::launch_apply(p, s.stream);
         }
         if (e == hipSuccess) e = hipMemcpyAsync(s.pin_out, s.d_out, n * out_stride, hipMemcpyDeviceToHost, s.stream);
+        if (e == hipSuccess && s.hashed)
+            e = hipMemcpyAsync(s.pin_hash, s.d_hash, static_cast<size_t>(n) * s.rows * sizeof(int32_t),
+                               hipMemcpyDeviceToHost, s.stream);
         if (e == hipSuccess) e = hipLaunchHostFunc(s.stream, &Batcher::on_done, &s);
         return e;
     }
@@ -539,7 +567,7 @@ int run_host(const HostOp& op, size_t len)
     if (e == hipSuccess && prev != dev) e = hipSetDevice(dev);
     if (e != hipSuccess) return map_hip(e);
     rc = Batcher::kFallback;
-    if (batch_config().enabled.load() == 1 && !op.update && !op.lens && !op.hashes) {
+    if (batch_config().enabled.load() == 1) {
         Batcher* b = batcher(dev);
         rc = b ? b->submit(op, len) : ELECT_EC_ENOMEM;
     }

@@ -34,11 +34,12 @@ inline kern::Column col(const void* base, size_t stripe_stride, size_t offset)
     return c;
 }
 
-// One synchronous host-memory operation: `cols` host inputs -> `rows` host outputs.
+// One synchronous host-memory operation: `cols` host inputs -> `rows` host outputs,
+// out[r] = XOR_j coef[r*cols+j] * in[j] (a parity update is the product
+// [c_r, c_r, e_r] over [old, new, P...]).  Outputs may alias inputs.
 struct HostOp {
     int cols = 0;
     int rows = 0;
-    bool update = false;  // cols = 2 + rows: [old, new, P...]; else an apply
     const unsigned char* const* in = nullptr;
     unsigned char* const* out = nullptr;
     uint8_t coef[kern::kMaxRows * kern::kMaxCols] = {};

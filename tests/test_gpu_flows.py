@@ -209,3 +209,63 @@ def test_host_update_ex_empty_old(dev, oracle):
     want = oracle.Encoder(k, m).encode_update([np.zeros(L, np.uint8), new] + pin, t)
     for r in range(m):
         assert np.array_equal(out[r], want[r])
+
+
+def test_cross_thread_batching_fused_steps(dev, oracle):
+    """ELECT's coding threads issue the fused steps concurrently: padded / hashed /
+    both / neither encodes and updates are distinct batch shapes, so batches close
+    early and the arenas alternate; every caller must get its own parity and
+    hashes.  Plain encodeUpdate batches too (as a product)."""
+    import threading
+    from elect_amd import _lib
+    from elect_amd.coder import RSCoder
+    k, m = 4, 2
+    coder = RSCoder(k, m)
+    enc = oracle.Encoder(k, m)
+    errors = []
+    _lib.set_batching(True, window_us=300, arena_bytes=8 << 20)
+    try:
+        def worker(t):
+            try:
+                L = 65536 + 4 if t % 2 else 4099
+                padded, hashed = bool(t & 2), bool(t & 4)
+                rng = np.random.default_rng(2000 + t)
+                for it in range(3):
+                    d = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+                    lens = [int(x) for x in rng.integers(0, L + 1, k)] if padded else None
+                    p = [np.empty(L, np.uint8) for _ in range(m)]
+                    hs = coder.encode_ex_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L,
+                                              data_lengths=lens, hashed=hashed)
+                    full = [oracle.zero_fill(x[:n], L) for x, n in zip(d, lens)] if padded else d
+                    want = enc.encode(full)
+                    if not all(np.array_equal(a, b) for a, b in zip(p, want)):
+                        errors.append(f"t{t} it{it} encode")
+                    if hashed and hs != [oracle.java_hashcode(w) for w in want]:
+                        errors.append(f"t{t} it{it} encode hashes")
+                    tgt = it % k
+                    new = rng.integers(0, 256, L, dtype=np.uint8)
+                    ul = [lens[tgt], int(rng.integers(0, L + 1))] if padded else None
+                    ins = [d[tgt].ctypes.data, new.ctypes.data] + [x.ctypes.data for x in p]
+                    if padded or hashed:
+                        hs = coder.encode_update_ex_host(ins, tgt, [x.ctypes.data for x in p], L,
+                                                         old_new_lengths=ul, hashed=hashed)
+                    else:
+                        coder.encode_update_host(ins, tgt, [x.ctypes.data for x in p], L)
+                    full = list(full)
+                    full[tgt] = oracle.zero_fill(new[:ul[1]], L) if padded else new
+                    want = enc.encode(full)
+                    if not all(np.array_equal(a, b) for a, b in zip(p, want)):
+                        errors.append(f"t{t} it{it} update")
+                    if hashed and hs != [oracle.java_hashcode(w) for w in want]:
+                        errors.append(f"t{t} it{it} update hashes")
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(24)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    finally:
+        _lib.set_batching(True)
+    assert not errors, errors[:5]
