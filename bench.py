@@ -565,66 +565,76 @@ def config_hashed(args, world, rank, dev):
 
 
 def config_flows(args, world, rank, dev):
-    """ELECT's two coding-node steps as it runs them, each one fused launch:
+    """ELECT's three coding-node steps as it runs them, each one fused launch:
     transition encode (ECMessageVerbHandler.java:283-329: zero fill to codeLength,
-    encode, parity hashCode) and parity update (ECParityUpdateVerbHandler.java:
-    634-699: old/new zero filled, encodeUpdate in place, new-parity hashCode).
-    RS(6,4), codeLength --chunk, 4096 stripes per GPU; contents fill
-    1/1.05 of codeLength less up to 5 % (codeLength = ceil(1.05 x SSTable size),
-    StorageService.java:331-339)."""
-    from elect_amd.batch import encode_batch, encode_batch_ex, encode_update_batch_ex
+    encode, parity hashCode), parity update (ECParityUpdateVerbHandler.java:
+    634-699: old/new zero filled, encodeUpdate in place, new-parity hashCode) and
+    degraded read (ECRecovery.java:128-141: survivors zero filled, decode of the
+    updated unit).  RS(6,4), codeLength --chunk, --stripes per GPU in one
+    [B][k+m][L] block; contents fill 1/1.05 of codeLength less up to 5 %
+    (codeLength = ceil(1.05 x SSTable size), StorageService.java:331-339)."""
+    from elect_amd.batch import decode_batch_ex, encode_batch, encode_batch_ex, encode_update_batch_ex
     from elect_amd.coder import RSCoder, java_bytebuffer_hash
     k, m, L, B = 4, 2, args.chunk, args.stripes
     coder = RSCoder(k, m)
     g = torch.Generator(device=dev)
     g.manual_seed(0xE1EC7)
-    data = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g)
+    stripe = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
+    data, par = stripe[:, :k], stripe[:, k:]
+    data.copy_(torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g))
     top = int(L / 1.05)
     lens = torch.randint(int(top * 0.95), top + 1, (B, k), dtype=torch.int32, device=dev, generator=g)
     new = torch.randint(0, 256, (B, L), dtype=torch.uint8, device=dev, generator=g)
     t = 1
     ulens = torch.stack([lens[:, t], torch.randint(int(top * 0.95), top + 1, (B,), dtype=torch.int32, device=dev,
                                                    generator=g)], dim=1).contiguous()
-    par = torch.empty((B, m, L), dtype=torch.uint8, device=dev)
+    surv = [j for j in range(k) if j != t] + [k]  # degraded read of unit t from the others + parity 0
+    dlens = torch.cat([lens[:, [j for j in range(k) if j != t]],
+                       torch.full((B, 1), L, dtype=torch.int32, device=dev)], dim=1).contiguous()
+    rebuilt = torch.empty((B, 1, L), dtype=torch.uint8, device=dev)
     h_enc = torch.empty((B, m), dtype=torch.int32, device=dev)
     h_upd = torch.empty((B, m), dtype=torch.int32, device=dev)
-    ev = {"encode": [], "update": []}
+    ev = {"encode": [], "update": [], "decode": []}
 
     def step():
-        es = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        es = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         es[0].record()
         encode_batch_ex(coder, data, par, lengths=lens, hashes=h_enc)
         es[1].record()
         encode_update_batch_ex(coder, t, data[:, t], new, par, par, lengths=ulens, hashes=h_upd)
         es[2].record()
-        ev["encode"].append((es[0], es[1]))
-        ev["update"].append((es[1], es[2]))
+        decode_batch_ex(coder, stripe, surv, [t], rebuilt, lengths=dlens, inputs_by_unit=True)
+        es[3].record()
+        for i, n in enumerate(("encode", "update", "decode")):
+            ev[n].append((es[i], es[i + 1]))
 
     dt = timed(step, args.steps, args.warmup, world)
     ms = {n: sum(a.elapsed_time(b) for a, b in v[-args.steps:]) / args.steps for n, v in ev.items()}
-    # self-check through the product: the updated parity is the encode of the new zero-filled stripe
+    # self-check through the product: the updated parity is the encode of the new zero-filled
+    # stripe, its hashes match, and the degraded read returns the new unit zero filled
     idx = torch.arange(L, device=dev).view(1, L)
     zero = torch.zeros((), dtype=torch.uint8, device=dev)
     filled = torch.where(idx.view(1, 1, L) < lens.view(B, k, 1), data, zero)
     filled[:, t] = torch.where(idx < ulens[:, 1:2], new, zero)
-    encode_batch_ex(coder, data, par, lengths=lens, hashes=h_enc)
-    encode_update_batch_ex(coder, t, data[:, t], new, par, par, lengths=ulens, hashes=h_upd)
     ref = torch.empty_like(par)
     encode_batch(coder, filled, ref)
     h = h_upd.cpu()
     ok = torch.equal(par, ref) and all(int(h[s, r]) == java_bytebuffer_hash(ref[s, r].cpu().numpy())
                                        for s, r in ((0, 0), (B - 1, m - 1)))
+    ok = ok and torch.equal(rebuilt[:, 0], filled[:, t])
     valid = int(lens.sum().item())
     uvalid = int(ulens.sum().item())
-    alg = {"encode": valid + B * m * L, "update": uvalid + 2 * B * m * L}
+    dvalid = int(dlens.sum().item())
+    alg = {"encode": valid + B * m * L, "update": uvalid + 2 * B * m * L, "decode": dvalid + B * L}
     kern = {}
-    for n in ("encode", "update"):
+    for n in ("encode", "update", "decode"):
         gbs = alg[n] / (ms[n] * 1e-3) / 1e9
         kern[n] = {"ms": round(ms[n], 4), "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                    "algorithmic_bytes_per_launch": alg[n]}
-    return {"metric": "GiB/s device-resident ELECT coding steps (padded+hashed encode, padded+hashed update), RS(6,4)",
-            "value": round(world * args.steps * B * (k + 1) * L / dt / GIB, 2),
-            "unit": "GiB/s (codeLength bytes: k units encoded + 1 unit updated per stripe)",
+    return {"metric": "GiB/s device-resident ELECT coding steps (padded+hashed encode, padded+hashed update, "
+                      "padded degraded-read decode), RS(6,4)",
+            "value": round(world * args.steps * B * (2 * k + 1) * L / dt / GIB, 2),
+            "unit": "GiB/s (codeLength bytes: k units encoded + 1 updated + k survivors decoded per stripe)",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok, "kernels": kern,
@@ -633,8 +643,8 @@ def config_flows(args, world, rank, dev):
                          "kernel": "gf_apply_x16<4,2,PAD,HASH> (encode step)",
                          "algorithmic_bytes_per_launch": alg["encode"],
                          "fill": round(valid / (B * k * L), 3)},
-            "config": {"workload": f"{B} stripes x {L} B codeLength per GPU; encode all, then update unit {t} "
-                                   "in place", "parallelism": f"stripe-partitioned x{world}"}}
+            "config": {"workload": f"{B} stripes x {L} B codeLength per GPU; encode all, update unit {t} in place, "
+                                   f"rebuild unit {t} from units {surv}", "parallelism": f"stripe-partitioned x{world}"}}
 
 
 def main():

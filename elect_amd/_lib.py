@@ -89,6 +89,8 @@ SIGNATURES = [
                                                  _u8pp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32)]),
     ("elect_ec_decode", ctypes.c_int, [_cp, _u8pp, _ip, _ip, ctypes.c_int, _u8pp, ctypes.c_size_t,
                                        ctypes.c_int]),
+    ("elect_ec_decode_ex", ctypes.c_int, [_cp, _u8pp, ctypes.POINTER(ctypes.c_size_t), _ip, _ip, ctypes.c_int,
+                                          _u8pp, ctypes.c_size_t, ctypes.c_int]),
     ("elect_ec_encode_batch", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, Shards, Shards, _cp]),
     ("elect_ec_decode_batch", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, Shards, _ip, _ip,
                                              ctypes.c_int, Shards, ctypes.c_uint, ctypes.c_int, _cp]),
@@ -102,6 +104,8 @@ SIGNATURES = [
                                                 _cp, _cp]),
     ("elect_ec_encode_update_batch_ex", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                                                        ColumnT, ColumnT, _cp, Shards, Shards, _cp, _cp]),
+    ("elect_ec_decode_batch_ex", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, Shards, _cp, _ip, _ip,
+                                                ctypes.c_int, Shards, ctypes.c_uint, ctypes.c_int, _cp]),
     ("elect_ec_apply_batch", ctypes.c_int, [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
                                             ctypes.c_size_t, ctypes.POINTER(ColumnT),
                                             ctypes.POINTER(ColumnT), _cp]),

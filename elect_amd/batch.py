@@ -84,6 +84,21 @@ def decode_batch(coder: RSCoder, inputs: torch.Tensor, decode_indexes, erased, o
                                            _stream(stream)), "decode_batch")
 
 
+def decode_batch_ex(coder: RSCoder, inputs: torch.Tensor, decode_indexes, erased, outputs: torch.Tensor,
+                    lengths=None, mode: int = _lib.DECODE_COMPAT, inputs_by_unit: bool = False,
+                    outputs_by_unit: bool = False, stream=None) -> int:
+    """decode_batch over zero-padded survivors (ECRecovery.java:128-141): lengths[s, j] content
+    bytes of survivor j (decode_indexes order; int32 device tensor [B, k], each <= L)."""
+    B, _, L = inputs.shape
+    flags = (_lib.INPUTS_BY_UNIT if inputs_by_unit else 0) | (_lib.OUTPUTS_BY_UNIT if outputs_by_unit else 0)
+    if len(decode_indexes) != coder.k:
+        raise ValueError("decode_indexes needs exactly k entries")
+    return check(lib.elect_ec_decode_batch_ex(coder.handle, L, B, _shards(inputs),
+                                              _lengths(lengths, B, coder.k, inputs.device),
+                                              int_array(decode_indexes), int_array(erased), len(erased),
+                                              _shards(outputs), flags, mode, _stream(stream)), "decode_batch_ex")
+
+
 def encode_update_batch(coder: RSCoder, target: int, old: torch.Tensor, new: torch.Tensor,
                         parity_in: torch.Tensor, parity_out: torch.Tensor, stream=None) -> None:
     """parity_out[s, r] = parity_in[s, r] ^ E[k+r][target] * (old[s] ^ new[s]); in place allowed."""

@@ -286,6 +286,19 @@ class RSCoder:
         return check(lib.elect_ec_encode_update(self.handle, ptr_array(in_addrs), target,
                                                 ptr_array(out_addrs), length), "encodeUpdate")
 
+    def decode_ex_host(self, in_addrs, decode_indexes, erased, out_addrs, length: int, input_lengths=None,
+                       mode: int = _lib.DECODE_COMPAT) -> int:
+        """ELECT's degraded-read decode (ECRecovery.java:128-149): survivor j holds
+        input_lengths[j] content bytes (zero past them; None address for an empty one);
+        `length` may be just the prefix of the rebuilt units the caller needs."""
+        lens = None
+        if input_lengths is not None:
+            lens = (_lib.ctypes.c_size_t * len(input_lengths))(*[int(x) for x in input_lengths])
+        addrs = [a if a is not None else 0 for a in in_addrs]
+        return check(lib.elect_ec_decode_ex(self.handle, ptr_array(addrs), lens, int_array(decode_indexes),
+                                            int_array(erased), len(erased), ptr_array(out_addrs), length, mode),
+                     "decode_ex")
+
     def decode_host(self, in_addrs, decode_indexes, erased, out_addrs, length: int,
                     mode: int = _lib.DECODE_COMPAT) -> int:
         return check(lib.elect_ec_decode(self.handle, ptr_array(in_addrs), int_array(decode_indexes),

@@ -279,7 +279,16 @@ int elect_ec_decode(const elect_ec_coder* coder, const unsigned char* const* inp
                     const int* erased_indexes, int num_erased, unsigned char* const* outputs, size_t chunk_size,
                     int mode)
 {
+    return elect_ec_decode_ex(coder, inputs, nullptr, decode_indexes, erased_indexes, num_erased, outputs,
+                              chunk_size, mode);
+}
+
+int elect_ec_decode_ex(const elect_ec_coder* coder, const unsigned char* const* inputs, const size_t* input_lengths,
+                       const int* decode_indexes, const int* erased_indexes, int num_erased,
+                       unsigned char* const* outputs, size_t chunk_size, int mode)
+{
     if (!valid_coder(coder) || !inputs || (num_erased > 0 && !outputs)) return ELECT_EC_EINVAL;
+    if (input_lengths && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
     HostOp op;
     const int st = build_decode_matrix(coder, decode_indexes, erased_indexes, num_erased, mode, op.coef);
     if (st < 0) return st;
@@ -288,6 +297,11 @@ int elect_ec_decode(const elect_ec_coder* coder, const unsigned char* const* inp
     op.rows = num_erased;
     op.in = inputs;
     op.out = outputs;
+    size_t lens[ELECT_EC_MAX_DATA_UNITS];
+    if (input_lengths) {  // content past chunk_size is not needed for a chunk_size prefix
+        for (int j = 0; j < coder->k; ++j) lens[j] = std::min(input_lengths[j], chunk_size);
+        op.lens = lens;
+    }
     const int rc = run_host(op, chunk_size);
     return rc != ELECT_EC_OK ? rc : st;
 }
@@ -362,7 +376,17 @@ int elect_ec_decode_batch(const elect_ec_coder* coder, size_t chunk_size, size_t
                           elect_ec_shards inputs, const int* decode_indexes, const int* erased_indexes,
                           int num_erased, elect_ec_shards outputs, unsigned flags, int mode, void* stream)
 {
+    return elect_ec_decode_batch_ex(coder, chunk_size, num_stripes, inputs, nullptr, decode_indexes, erased_indexes,
+                                    num_erased, outputs, flags, mode, stream);
+}
+
+int elect_ec_decode_batch_ex(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                             elect_ec_shards inputs, const uint32_t* d_input_lengths, const int* decode_indexes,
+                             const int* erased_indexes, int num_erased, elect_ec_shards outputs, unsigned flags,
+                             int mode, void* stream)
+{
     if (!valid_coder(coder)) return ELECT_EC_EINVAL;
+    if (d_input_lengths && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
     ApplyParams p;
     const int st = build_decode_matrix(coder, decode_indexes, erased_indexes, num_erased, mode, p.coef);
     if (st < 0) return st;
@@ -379,6 +403,10 @@ int elect_ec_decode_batch(const elect_ec_coder* coder, size_t chunk_size, size_t
     for (int r = 0; r < p.rows; ++r) {
         const size_t slot = (flags & ELECT_EC_OUTPUTS_BY_UNIT) ? static_cast<size_t>(erased_indexes[r]) : r;
         p.dst[r] = col(outputs.base, outputs.stripe_stride, slot * outputs.shard_stride);
+    }
+    if (d_input_lengths) {
+        p.padded = true;
+        p.lens = d_input_lengths;
     }
     const int rc = map_hip(elect::kern::launch_apply(p, as_stream(stream)));
     return rc != ELECT_EC_OK ? rc : st;

@@ -7,9 +7,9 @@
  * EC/NativeRSDecoder.c:32-82) and forwards them to the MI355X C ABI
  * (include/elect_ec.h).  Built only where a JDK provides <jni.h>; see
  * INTEGRATION.md for the build line.  No Java code changes: ELECT keeps calling
- * System.loadLibrary("ec") (JEC/NativeRSEncoder.java:37).  Two optional
- * methods (encodeExImpl, encodeUpdateExImpl) expose the fused coding-node
- * steps to a Java that declares them.
+ * System.loadLibrary("ec") (JEC/NativeRSEncoder.java:37).  Three optional
+ * methods (encodeExImpl, encodeUpdateExImpl, decodeExImpl) expose the fused
+ * coding-node steps to a Java that declares them.
  *
  * Differences from the reference glue, all on error paths:
  *  - every THROW returns (EC/NativeRSDecoder.c:50-52 and EC/jni_common.c:70-73,
@@ -338,6 +338,45 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_decodeImpl(JNIEnv* env,
                  elect_ec_decode(c, (const unsigned char* const*)in, dec, era, n_era, out, (size_t)dataLen,
                                  decode_mode()),
                  "decode");
+}
+
+/* optional: ECRecovery's degraded-read decode (:128-149) with survivors zero
+ * padded past contentLengths (k entries, decodeIndexes order; null = all full)
+ * and dataLen possibly just the prefix the caller keeps. */
+JNIEXPORT void JNICALL
+Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_decodeExImpl(JNIEnv* env, jobject thiz,
+                                                                      jobjectArray inputs, jintArray inputOffsets,
+                                                                      jintArray contentLengths, jint dataLen,
+                                                                      jintArray decodeIndexes, jintArray erasedIndexes,
+                                                                      jobjectArray outputs, jintArray outputOffsets)
+{
+    unsigned char* in[2 + EC_MAX];
+    unsigned char* out[2 + EC_MAX];
+    int dec[EC_MAX], era[EC_MAX];
+    size_t lens[EC_MAX];
+    const size_t* use_lens;
+    elect_ec_coder* c = get_coder(env, thiz);
+    if (c == NULL) {
+        throw_java(env, "java/io/IOException", "NativeRSRawDecoder closed");
+        return;
+    }
+    int k = elect_ec_coder_num_data_units(c);
+    int n_dec = (*env)->GetArrayLength(env, decodeIndexes);
+    int n_era = (*env)->GetArrayLength(env, erasedIndexes);
+    if (n_dec < k || n_era > EC_MAX) {
+        throw_java(env, "java/lang/InternalError", "Invalid decode/erased indexes");
+        return;
+    }
+    (*env)->GetIntArrayRegion(env, decodeIndexes, 0, k, (jint*)dec);
+    (*env)->GetIntArrayRegion(env, erasedIndexes, 0, n_era, (jint*)era);
+    if (buffers(env, inputs, inputOffsets, k, in, "Invalid inputs") ||
+        buffers(env, outputs, outputOffsets, n_era, out, "Invalid outputs") ||
+        content_lengths(env, contentLengths, k, lens, &use_lens))
+        return;
+    raise_status(env,
+                 elect_ec_decode_ex(c, (const unsigned char* const*)in, use_lens, dec, era, n_era, out,
+                                    (size_t)dataLen, decode_mode()),
+                 "decodeEx");
 }
 
 JNIEXPORT void JNICALL

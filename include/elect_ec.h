@@ -180,6 +180,16 @@ int elect_ec_encode_ex(const elect_ec_coder* coder, const unsigned char* const* 
 int elect_ec_encode_update_ex(const elect_ec_coder* coder, const unsigned char* const* old_new_parity,
                               const size_t* old_new_lengths, int target_data_index,
                               unsigned char* const* new_parity_units, size_t chunk_size, int32_t* hashes);
+/* decode_ex is the degraded-read decode of JEC/net/ECRecovery.java:128-149: each
+ * survivor holds input_lengths[j] content bytes (NULL = all full) and reads as
+ * zero past them (ELECT copies survivors into zero-filled codeLength buffers,
+ * :130-133).  chunk_size may be only the prefix the caller needs (ECRecovery
+ * keeps dataFileSize bytes of the rebuilt unit, :146-149): RS works bytewise,
+ * so a prefix decode reads only that prefix of each survivor.  Lengths above
+ * chunk_size are clamped to it. */
+int elect_ec_decode_ex(const elect_ec_coder* coder, const unsigned char* const* inputs,
+                       const size_t* input_lengths, const int* decode_indexes, const int* erased_indexes,
+                       int num_erased, unsigned char* const* outputs, size_t chunk_size, int mode);
 
 /* ---- device resident, batched, stream ordered ----
  * Many stripes per launch.  All pointers are device pointers on the calling
@@ -223,6 +233,12 @@ int elect_ec_encode_update_batch_ex(const elect_ec_coder* coder, size_t chunk_si
                                     int target_data_index, elect_ec_column old_data, elect_ec_column new_data,
                                     const uint32_t* d_old_new_lengths, elect_ec_shards parity_in,
                                     elect_ec_shards parity_out, int32_t* d_hashes, void* stream);
+/* decode_batch with survivors zero padded: d_input_lengths is a DEVICE uint32
+ * [num_stripes][k] array in decode_indexes order, each <= chunk_size. */
+int elect_ec_decode_batch_ex(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
+                             elect_ec_shards inputs, const uint32_t* d_input_lengths, const int* decode_indexes,
+                             const int* erased_indexes, int num_erased, elect_ec_shards outputs,
+                             unsigned flags, int mode, void* stream);
 /* General product dst[r] = XOR_j coef[r*cols+j] * src[j], rows, cols <= 16. */
 int elect_ec_apply_batch(const unsigned char* coef, int rows, int cols, size_t chunk_size,
                          size_t num_stripes, const elect_ec_column* src,

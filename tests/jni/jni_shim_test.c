@@ -250,6 +250,8 @@ typedef void (*encode_ex_fn)(JNIEnv*, jobject, jobjectArray, jintArray, jintArra
                              jintArray);
 typedef void (*update_ex_fn)(JNIEnv*, jobject, jobjectArray, jintArray, jintArray, jint, jint, jobjectArray,
                              jintArray, jintArray);
+typedef void (*decode_ex_fn)(JNIEnv*, jobject, jobjectArray, jintArray, jintArray, jint, jintArray, jintArray,
+                             jobjectArray, jintArray);
 typedef void (*decode_fn)(JNIEnv*, jobject, jobjectArray, jintArray, jint, jintArray, jintArray, jobjectArray,
                           jintArray);
 
@@ -261,6 +263,7 @@ static struct {
     destroy_fn enc_destroy, dec_destroy;
     encode_ex_fn encode_ex;
     update_ex_fn update_ex;
+    decode_ex_fn decode_ex;
     int (*device_count)(int*);
 } jni;
 
@@ -291,6 +294,7 @@ static void load(const char* lib)
     jni.dec_destroy = (destroy_fn)sym(h, PFX "NativeRSDecoder_destroyImpl");
     jni.encode_ex = (encode_ex_fn)sym(h, PFX "NativeRSEncoder_encodeExImpl");
     jni.update_ex = (update_ex_fn)sym(h, PFX "NativeRSEncoder_encodeUpdateExImpl");
+    jni.decode_ex = (decode_ex_fn)sym(h, PFX "NativeRSDecoder_decodeExImpl");
     jni.device_count = (int (*)(int*))sym(h, "elect_ec_device_count");
 }
 
@@ -460,6 +464,13 @@ static int cpu_checks(void)
     const jint er_bad[1] = {7};  /* engine-side validation (unit 7 of 6) surfaces as a Java exception */
     jni.decode(env, dec, in4, off4, 16, int_array(4, di4), int_array(1, er_bad), out1, poff1);
     EXPECT(threw("java/lang/IllegalArgumentException", "invalid argument"));
+    const jint dl3[3] = {16, 16, 16}, dl4[4] = {16, 3, -2, 16};
+    jni.decode_ex(env, dec, in4, off4, int_array(3, dl3), 16, int_array(4, di4), int_array(1, er1), out1, poff1);
+    EXPECT(threw("java/lang/InternalError", "Invalid content lengths"));
+    jni.decode_ex(env, dec, in4, off4, int_array(4, dl4), 16, int_array(4, di4), int_array(1, er1), out1, poff1);
+    EXPECT(threw("java/lang/IllegalArgumentException", "negative content length"));
+    jni.decode_ex(env, dec, in4, off4, NULL, 16, int_array(3, di3), int_array(1, er1), out1, poff1);
+    EXPECT(threw("java/lang/InternalError", "Invalid decode/erased indexes"));
 
     /* an object without the nativeCoder field -> UnsatisfiedLinkError (EC/jni_common.h:29-36) */
     jobject alien = coder_obj("java/lang/Object");
@@ -470,6 +481,8 @@ static int cpu_checks(void)
     EXPECT(clean());
     EXPECT(dec->native_coder == 0);
     jni.decode(env, dec, in4, off4, 16, int_array(4, di4), int_array(1, er1), out1, poff1);
+    EXPECT(threw("java/io/IOException", "NativeRSRawDecoder closed"));
+    jni.decode_ex(env, dec, in4, off4, NULL, 16, int_array(4, di4), int_array(1, er1), out1, poff1);
     EXPECT(threw("java/io/IOException", "NativeRSRawDecoder closed"));
 
     EXPECT(vm.violations == 0);
@@ -641,6 +654,23 @@ static int gpu_fused_flows(void)
         EXPECT(!memcmp(at(&par, r), at(&ref2, r), L));
         EXPECT(hashes->ints[r] == java_hash(at(&ref2, r), L));
     }
+    /* degraded read of unit 1 (new content, 5000 bytes) from [P0, d0, d2, d3]: the data
+     * survivors padded past their content, only the 5000-byte prefix decoded (ECRecovery) */
+    jobject dec = coder_obj(DEC_CLS);
+    jni.dec_init(env, dec, K, M);
+    struct Bufs rb;
+    bufs_init(&rb, 1, L, 7);
+    memset(at(&rb, 0), 0x33, L);
+    const jint di[K] = {4, 0, 2, 3}, er[1] = {1};
+    const jint dlens[K] = {L, lens[0], lens[2], lens[3]};
+    jobject din[K] = {par.bb[0], raw.bb[0], raw.bb[2], raw.bb[3]};
+    jint din_pos[K] = {par.pos[0], raw.pos[0], raw.pos[2], raw.pos[3]};
+    jni.decode_ex(env, dec, obj_array(K, din), int_array(K, din_pos), int_array(K, dlens), ulens[1], int_array(K, di),
+                  int_array(1, er), obj_array(1, rb.bb), int_array(1, rb.pos));
+    EXPECT(clean());
+    EXPECT(!memcmp(at(&rb, 0), at(&newd, 0), ulens[1]));
+    EXPECT(at(&rb, 0)[ulens[1]] == 0x33);  /* nothing past the requested prefix is written */
+    jni.dec_destroy(env, dec);
     jni.enc_destroy(env, enc);
     EXPECT(vm.violations == 0);
     EXPECT(vm.live_int_elems == 0);

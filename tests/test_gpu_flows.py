@@ -269,3 +269,64 @@ def test_cross_thread_batching_fused_steps(dev, oracle):
     finally:
         _lib.set_batching(True)
     assert not errors, errors[:5]
+
+
+DEC_CASES = [(4, 2, 65536), (4, 2, 4099), (4, 2, 1040), (8, 4, 2048), (3, 2, 17), (10, 4, 333)]
+
+
+@pytest.mark.parametrize("k,m,L", DEC_CASES)
+@pytest.mark.parametrize("n_erased", [1, 2])
+def test_decode_batch_ex_padded_survivors(dev, oracle, k, m, L, n_erased):
+    """ECRecovery's degraded read (:128-141): survivors copied into zero-filled codeLength
+    buffers.  Data survivors hold their content lengths (0xFF garbage past them), parity
+    survivors are full; strict and compat modes against the oracle's decode."""
+    from elect_amd import _lib
+    from elect_amd.batch import decode_batch_ex
+    from elect_amd.coder import RSCoder
+    rng = np.random.default_rng(L + 11 * k + n_erased)
+    B = 4
+    data = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    dlens = _lengths(rng, B, k, L)
+    enc = oracle.Encoder(k, m)
+    stripes = np.zeros((B, k + m, L), np.uint8)
+    for s in range(B):
+        full = [oracle.zero_fill(data[s, j, :dlens[s, j]], L) for j in range(k)]
+        stripes[s, :k] = np.stack(full)
+        stripes[s, k:] = np.stack(enc.encode(full))
+    erased = list(range(n_erased))                       # data units lost
+    surv = list(range(n_erased, k)) + list(range(k, k + n_erased))
+    lens = np.array([[dlens[s, u] if u < k else L for u in surv] for s in range(B)], np.int32)
+    stored = stripes.copy()
+    for s in range(B):
+        for u in range(k):
+            stored[s, u, dlens[s, u]:] = 0xFF
+    out = torch.full((B, n_erased, L), 0x44, dtype=torch.uint8, device=dev)
+    for mode in (_lib.DECODE_COMPAT, _lib.DECODE_STRICT):
+        decode_batch_ex(RSCoder(k, m), _to(dev, stored), surv, erased, out, lengths=_to(dev, lens), mode=mode,
+                        inputs_by_unit=True)
+        got = out.cpu().numpy()
+        for s in range(B):
+            for r, e in enumerate(erased):
+                assert np.array_equal(got[s, r], stripes[s, e]), (mode, s, r)
+
+
+def test_host_decode_ex_prefix(dev, oracle):
+    """elect_ec_decode_ex as ECRecovery would call it: only the dataFileSize prefix of the
+    rebuilt SSTable is decoded, from survivors shorter than codeLength (one empty, NULL)."""
+    from elect_amd.coder import RSCoder
+    k, m, L = 4, 2, 4404020
+    rng = np.random.default_rng(12)
+    lens = [L - 7, 3_000_001, 0, 4_404_000]
+    data = [oracle.zero_fill(rng.integers(0, 256, n, dtype=np.uint8), L) for n in lens]
+    par = oracle.Encoder(k, m).encode(data)
+    raw = [d.copy() for d in data]
+    for d, n in zip(raw, lens):
+        d[n:] = 0xEE
+    want_len = lens[1]
+    out = np.full(L, 0x33, np.uint8)
+    surv = [0, 2, 3, 4]  # unit 1 lost
+    addrs = [raw[0].ctypes.data, None, raw[3].ctypes.data, par[0].ctypes.data]
+    RSCoder(k, m).decode_ex_host(addrs, surv, [1], [out.ctypes.data], want_len,
+                                 input_lengths=[lens[0], 0, lens[3], L])
+    assert np.array_equal(out[:want_len], data[1][:want_len])
+    assert (out[want_len:] == 0x33).all()

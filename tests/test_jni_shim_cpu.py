@@ -13,6 +13,7 @@ from tests.jni_build import build
 OPTIONAL = {  # fused coding-node steps, bound only by a Java that declares them
     "Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeExImpl",
     "Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeUpdateExImpl",
+    "Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_decodeExImpl",
 }
 SEVEN = {
     "Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_initImpl",
@@ -25,7 +26,7 @@ SEVEN = {
 }
 
 
-def test_shim_exports_the_seven_native_methods_and_the_two_optional_ones():
+def test_shim_exports_the_seven_native_methods_and_the_three_optional_ones():
     lib, _ = build()
     out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
     exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
