@@ -261,6 +261,8 @@ struct FastArgs {
     uint32_t shift;
     // padded launches only
     uint64_t len;            // bytes per shard (the last segment may be partial)
+    uint32_t len32;          // min(len, 2^32-1): device lengths are clamped to it, so no load
+                             // leaves a unit whatever a caller's length array holds
     const uint32_t* lens;    // [stripe][lstride] content lengths of columns < lcols, or null -> clen
     uint32_t lstride;
     uint32_t lcols;          // columns >= lcols hold clen[j] valid bytes
@@ -356,7 +358,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         uniform = s0 == s1;
         const uint32_t* l = a.lens + static_cast<uint64_t>(s0) * a.lstride;
 #pragma unroll
-        for (int j = 0; j < K; ++j) sl[j] = j < a.lcols ? __builtin_amdgcn_readfirstlane(l[j]) : a.clen[j];
+        for (int j = 0; j < K; ++j) sl[j] = j < a.lcols ? min(__builtin_amdgcn_readfirstlane(l[j]), a.len32) : a.clen[j];
     }
 
     stage_tables(a, tl);
@@ -377,7 +379,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         } else {  // all lengths first: vmcnt is in order, so interleaving would serialise
             const uint32_t* l = a.lens + static_cast<uint64_t>(stripe) * a.lstride;
 #pragma unroll
-            for (int j = 0; j < K; ++j) valid[j] = j < a.lcols ? l[j] : a.clen[j];
+            for (int j = 0; j < K; ++j) valid[j] = j < a.lcols ? min(l[j], a.len32) : a.clen[j];
         }
         // Full segments first (no loads at all past a column's content length),
         // then the one segment per unit that holds the content end, loaded whole
@@ -486,7 +488,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
         uniform = s0 == stripe_of(min(first + 64u * U - 1u, a.total - 1u));
         const uint32_t* l = a.lens + static_cast<uint64_t>(s0) * a.lstride;
 #pragma unroll
-        for (int j = 0; j < K; ++j) sl[j] = j < a.lcols ? __builtin_amdgcn_readfirstlane(l[j]) : a.clen[j];
+        for (int j = 0; j < K; ++j) sl[j] = j < a.lcols ? min(__builtin_amdgcn_readfirstlane(l[j]), a.len32) : a.clen[j];
     }
     stage_tables(a, tl);
     if (first >= a.total) return;
@@ -547,7 +549,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
         const uint32_t* l = a.lens + static_cast<uint64_t>(stripe) * a.lstride;
         uint32_t valid[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) valid[j] = j < a.lcols ? l[j] : a.clen[j];
+        for (int j = 0; j < K; ++j) valid[j] = j < a.lcols ? min(l[j], a.len32) : a.clen[j];
         uint4 x[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
@@ -627,6 +629,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     a.magic = mg.m;
     a.shift = mg.p;
     a.len = p.len;
+    a.len32 = static_cast<uint32_t>(std::min<uint64_t>(p.len, 0xFFFFFFFFu));
     a.lstride = p.lens_stride ? p.lens_stride : static_cast<uint32_t>(p.cols);
     a.lcols = static_cast<uint32_t>(p.lens_cols ? p.lens_cols : p.cols);
     for (int j = 0; j < K; ++j) a.clen[j] = p.clen[j];

@@ -203,9 +203,10 @@ int elect_ec_decode_batch(const elect_ec_coder* coder, size_t chunk_size, size_t
                           const int* erased_indexes, int num_erased, elect_ec_shards outputs,
                           unsigned flags, int mode, void* stream);
 /* Zero-padded batch encode: data_lengths is a DEVICE array [num_stripes][k] of
- * uint32 content lengths (each <= chunk_size); bytes past a unit's length read
- * as zero whatever the buffer holds there.  Loads stop at the 16-byte segment
- * holding a unit's last content byte (always inside its chunk_size bytes). */
+ * uint32 content lengths; bytes past a unit's length read as zero whatever the
+ * buffer holds there, and a length above chunk_size counts as chunk_size (so
+ * no load ever leaves a unit).  Loads stop at the 16-byte segment holding a
+ * unit's last content byte (always inside its chunk_size bytes). */
 int elect_ec_encode_batch_padded(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
                                  elect_ec_shards data, const uint32_t* data_lengths,
                                  elect_ec_shards parity, void* stream);
@@ -234,7 +235,8 @@ int elect_ec_encode_update_batch_ex(const elect_ec_coder* coder, size_t chunk_si
                                     const uint32_t* d_old_new_lengths, elect_ec_shards parity_in,
                                     elect_ec_shards parity_out, int32_t* d_hashes, void* stream);
 /* decode_batch with survivors zero padded: d_input_lengths is a DEVICE uint32
- * [num_stripes][k] array in decode_indexes order, each <= chunk_size. */
+ * [num_stripes][k] array in decode_indexes order (above chunk_size counts as
+ * chunk_size). */
 int elect_ec_decode_batch_ex(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
                              elect_ec_shards inputs, const uint32_t* d_input_lengths, const int* decode_indexes,
                              const int* erased_indexes, int num_erased, elect_ec_shards outputs,
