@@ -358,7 +358,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         uniform = s0 == s1;
         const uint32_t* l = a.lens + static_cast<uint64_t>(s0) * a.lstride;
 #pragma unroll
-        for (int j = 0; j < K; ++j) sl[j] = j < a.lcols ? min(__builtin_amdgcn_readfirstlane(l[j]), a.len32) : a.clen[j];
+        for (int j = 0; j < K; ++j) sl[j] = j < a.lcols ? min(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(l[j])), a.len32) : a.clen[j];
     }
 
     stage_tables(a, tl);
@@ -488,7 +488,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
         uniform = s0 == stripe_of(min(first + 64u * U - 1u, a.total - 1u));
         const uint32_t* l = a.lens + static_cast<uint64_t>(s0) * a.lstride;
 #pragma unroll
-        for (int j = 0; j < K; ++j) sl[j] = j < a.lcols ? min(__builtin_amdgcn_readfirstlane(l[j]), a.len32) : a.clen[j];
+        for (int j = 0; j < K; ++j) sl[j] = j < a.lcols ? min(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(l[j])), a.len32) : a.clen[j];
     }
     stage_tables(a, tl);
     if (first >= a.total) return;

@@ -338,23 +338,27 @@ def test_device_lengths_above_chunk_count_as_full(dev, oracle):
     kernel (L % 16 != 0, hashed), gf_apply_lens (L % 16 == 0) and the padded decode."""
     from elect_amd.batch import decode_batch_ex, encode_batch_ex
     from elect_amd.coder import RSCoder
-    k, m, B = 4, 2, 3
-    for L, hashed in ((4099, True), (65536, False)):
+    k, m = 4, 2
+    for L, hashed, B in ((4099, True, 3), (65536, False, 3), ((20 << 20) + 4, True, 2)):
         rng = np.random.default_rng(L)
         data = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
         lens = np.full((B, k), 0xFFFFFFFF, np.uint32).view(np.int32)
         lens[1, 2] = L + 1
+        lens[1, 3] = L - 3  # beyond 2^24: lengths must stay exact integers on the device
         par = torch.empty((B, m, L), dtype=torch.uint8, device=dev)
         hs = torch.empty((B, m), dtype=torch.int32, device=dev) if hashed else None
         d_data = _to(dev, data)
         encode_batch_ex(RSCoder(k, m), d_data, par, lengths=_to(dev, lens), hashes=hs)
         enc = oracle.Encoder(k, m)
         for s in range(B):
-            want = enc.encode([data[s, j] for j in range(k)])
+            want = enc.encode([oracle.zero_fill(data[s, j, :min(int(lens[s, j]) & 0xFFFFFFFF, L)], L)
+                               for j in range(k)])
             for r in range(m):
                 assert np.array_equal(par[s, r].cpu().numpy(), want[r])
                 if hashed:
                     assert int(hs[s, r]) == oracle.java_hashcode(want[r])
+        if L > 1 << 24:
+            continue
         stripe = torch.cat([d_data, par], dim=1)
         out = torch.empty((B, 1, L), dtype=torch.uint8, device=dev)
         decode_batch_ex(RSCoder(k, m), stripe, [1, 2, 3, 4], [0], out, lengths=_to(dev, lens), inputs_by_unit=True)
