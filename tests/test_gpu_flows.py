@@ -361,5 +361,6 @@ def test_device_lengths_above_chunk_count_as_full(dev, oracle):
             continue
         stripe = torch.cat([d_data, par], dim=1)
         out = torch.empty((B, 1, L), dtype=torch.uint8, device=dev)
-        decode_batch_ex(RSCoder(k, m), stripe, [1, 2, 3, 4], [0], out, lengths=_to(dev, lens), inputs_by_unit=True)
-        assert torch.equal(out[:, 0], d_data[:, 0])
+        dl = np.concatenate([lens[:, 1:], np.full((B, 1), -1, np.int32)], axis=1)  # survivors 1, 2, 3, P0
+        decode_batch_ex(RSCoder(k, m), stripe, [1, 2, 3, 4], [0], out, lengths=_to(dev, dl), inputs_by_unit=True)
+        assert torch.equal(out[:, 0], d_data[:, 0])  # unit 0's lengths are all above L: full

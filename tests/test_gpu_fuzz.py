@@ -1,0 +1,140 @@
+"""Randomised GPU-vs-oracle cases over the whole device API surface.
+
+Each case draws a code (k, m), a chunk length (odd, multiple of 16, around the
+kernel thresholds), a stripe count, a byte offset (aligned or not), a stripe
+stride with slack, and optional content lengths (including 0, full, above
+the chunk) and hashes, then checks encode_batch_ex, encode_update_batch_ex
+and decode_batch_ex (random erasures, compat and strict) byte for byte
+against the oracle (L1 restatement, JDK hashCode loop, zero fill).  Seeded:
+a failure names its case number and reproduces.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CASES = 40
+
+
+def _case(i):
+    rng = np.random.default_rng(0xF00D + i)
+    k = int(rng.integers(1, 11))
+    m = int(rng.integers(1, min(8, 14 - k) + 1))
+    L = int(rng.choice([1, 15, 16, 17, 63, 1023, 1024, 1040, 4096, 4099, 16384 + 16 * int(rng.integers(0, 9)),
+                        65536, 65536 + 4, 70001]))
+    B = int(rng.integers(1, 7))
+    offset = int(rng.choice([0, 0, 16, 1, 3, 8]))
+    slack = int(rng.choice([0, 0, 16, 256, 5]))
+    return rng, k, m, L, B, offset, slack
+
+
+def _lengths(rng, B, n, L):
+    choice = rng.integers(0, 5, size=(B, n))
+    lens = rng.integers(0, L + 1, size=(B, n)).astype(np.int64)
+    lens[choice == 0] = 0
+    lens[choice == 1] = L
+    lens[choice == 2] = L + 1 + rng.integers(0, 1000, size=(choice == 2).sum())  # counts as L
+    return lens.astype(np.uint32).view(np.int32)
+
+
+def _clip(lens, L):
+    return np.minimum(lens.view(np.uint32).astype(np.int64), L)
+
+
+def _place(dev, a, offset, slack):
+    """A [B, n, L] device view of a at a byte offset, stripes `slack` bytes apart."""
+    B, n, L = a.shape
+    stride = n * L + slack
+    big = torch.zeros(offset + B * stride + 64, dtype=torch.uint8, device=dev)
+    view = big[offset:offset + B * stride].view(B, stride)[:, :n * L].view(B, n, L)
+    view.copy_(torch.from_numpy(np.ascontiguousarray(a)).to(dev))
+    return view
+
+
+@pytest.mark.parametrize("i", range(CASES))
+def test_fuzz_case(dev, oracle, i):
+    from elect_amd import _lib
+    from elect_amd.batch import decode_batch_ex, encode_batch_ex, encode_update_batch_ex
+    from elect_amd.coder import RSCoder
+    rng, k, m, L, B, offset, slack = _case(i)
+    c = RSCoder(k, m)
+    enc = oracle.Encoder(k, m)
+    data = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    padded = bool(rng.integers(0, 2))
+    hashed = bool(rng.integers(0, 2)) and m <= 8
+    lens = _lengths(rng, B, k, L) if padded else None
+    eff = _clip(lens, L) if padded else np.full((B, k), L)
+    full = np.zeros_like(data)
+    for s in range(B):
+        for j in range(k):
+            full[s, j, :eff[s, j]] = data[s, j, :eff[s, j]]
+
+    # encode step
+    stripe = _place(dev, np.concatenate([data, np.full((B, m, L), 0x5A, np.uint8)], axis=1), offset, slack)
+    hs = torch.zeros((B, m), dtype=torch.int32, device=dev) if hashed else None
+    encode_batch_ex(c, stripe[:, :k], stripe[:, k:], lengths=torch.from_numpy(lens).to(dev) if padded else None,
+                    hashes=hs)
+    got = stripe.cpu().numpy()
+    want = [enc.encode([full[s, j] for j in range(k)]) for s in range(B)]
+    for s in range(B):
+        for r in range(m):
+            assert np.array_equal(got[s, k + r], want[s][r]), (i, "encode", s, r)
+            if hashed:
+                assert int(hs[s, r]) == oracle.java_hashcode(want[s][r]), (i, "hash", s, r)
+
+    # update step, in place on the stored parity
+    t = int(rng.integers(0, k))
+    new = rng.integers(0, 256, (B, L), dtype=np.uint8)
+    ul = _lengths(rng, B, 2, L) if padded else None
+    if padded:
+        ul[:, 0] = lens[:, t]  # the old content is what was encoded
+    new_dev = _place(dev, new[:, None, :], offset, slack)[:, 0]
+    hu = torch.zeros((B, m), dtype=torch.int32, device=dev) if hashed else None
+    encode_update_batch_ex(c, t, stripe[:, t], new_dev, stripe[:, k:], stripe[:, k:],
+                           lengths=torch.from_numpy(np.ascontiguousarray(ul)).to(dev) if padded else None, hashes=hu)
+    new_eff = _clip(ul[:, 1:2], L)[:, 0] if padded else np.full(B, L)
+    full2 = full.copy()
+    for s in range(B):
+        full2[s, t] = 0
+        full2[s, t, :new_eff[s]] = new[s, :new_eff[s]]
+    got = stripe.cpu().numpy()
+    want2 = [enc.encode([full2[s, j] for j in range(k)]) for s in range(B)]
+    for s in range(B):
+        for r in range(m):
+            assert np.array_equal(got[s, k + r], want2[s][r]), (i, "update", s, r)
+            if hashed:
+                assert int(hu[s, r]) == oracle.java_hashcode(want2[s][r]), (i, "update hash", s, r)
+
+    # degraded read: random erasures (<= m), random survivor order, both modes
+    units = list(range(k + m))
+    ne = int(rng.integers(1, m + 1))
+    erased = [int(x) for x in rng.permutation(units)[:ne]]
+    surv = [u for u in rng.permutation(units) if u not in erased][:k]
+    surv = [int(u) for u in surv]
+    # the stored stripe: data units hold full2 (zero filled) except unit t, which holds `new`
+    # unpadded in the device buffer only via new_dev; rebuild a clean stored copy instead
+    stored = np.concatenate([full2, np.stack([np.stack(w) for w in want2])], axis=1)
+    dlen = None
+    if padded:  # survivors' content lengths; garbage past them in the device copy
+        dlen = np.zeros((B, k), np.int32)
+        shown = stored.copy()
+        for s in range(B):
+            for jj, u in enumerate(surv):
+                n = int(rng.integers(0, L + 1)) if u < k else L
+                n = max(n, int(np.max(np.nonzero(stored[s, u])[0], initial=-1)) + 1)  # keep all non-zero bytes
+                dlen[s, jj] = n
+                shown[s, u, n:] = 0xEE
+        dev_stripe = _place(dev, shown, offset, slack)
+    else:
+        dev_stripe = _place(dev, stored, offset, slack)
+    for mode in (_lib.DECODE_COMPAT, _lib.DECODE_STRICT):
+        out = torch.full((B, ne, L), 0x11, dtype=torch.uint8, device=dev)
+        st = decode_batch_ex(c, dev_stripe, surv, erased, out, lengths=torch.from_numpy(dlen).to(dev) if padded else None,
+                             mode=mode, inputs_by_unit=True)
+        got = out.cpu().numpy()
+        for s in range(B):
+            rc, want_d = oracle.decode(k, m, [stored[s, u] for u in surv], surv, erased, strict=bool(mode))
+            assert (st == _lib.WARN_SINGULAR) == (rc == -1)
+            for r in range(ne):
+                assert np.array_equal(got[s, r], want_d[r]), (i, "decode", mode, s, r, surv, erased)
