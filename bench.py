@@ -43,8 +43,10 @@ def parse():
     ap.add_argument("--m", type=int, default=2)
     ap.add_argument("--chunk", type=int, default=65536)
     ap.add_argument("--stripes", type=int, default=4096)
-    ap.add_argument("--layout", choices=("stripe", "unit"), default="stripe",
-                    help="HBM layout of the stripes ([B][k+m][L] or [k+m][B][L]); headline and mixed")
+    ap.add_argument("--layout", choices=("auto", "stripe", "unit"), default="auto",
+                    help="HBM layout of the stripes ([B][k+m][L] or [k+m][B][L]); headline and mixed. auto: "
+                         "unit-major for chunks <= 4 KiB (a stripe-major wave would read and write one "
+                         "6 KiB region), stripe-major above")
     ap.add_argument("--decode-out", choices=("separate", "inplace"), default="separate",
                     help="headline decode target: a separate [B][1][L] buffer, or the erased unit's own slot")
     ap.add_argument("--rebuilt-rows", type=int, default=1,
@@ -240,6 +242,14 @@ def device_copy_rate(dev, nbytes=1 << 30, reps=5):
     return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
 
 
+def layout_for(args, L: int) -> str:
+    """HBM layout of a batch of L-byte chunks: --layout, or for "auto" unit-major
+    [k+m][B][L] when L <= 4 KiB and stripe-major [B][k+m][L] above."""
+    if args.layout != "auto":
+        return args.layout
+    return "unit" if L <= 4096 else "stripe"
+
+
 def timed(step, steps, warmup, world):
     for _ in range(warmup):
         step()
@@ -266,7 +276,7 @@ def config_mixed(args, world, rank, dev):
     for L in (1024, 4096, 1 << 20):
         total = (1 << 30) // (k * L)
         b, e = partition_by_bytes([k * L] * total, world, rank)
-        if args.layout == "unit":  # [k+m][B][L]: every unit column is one contiguous region
+        if layout_for(args, L) == "unit":  # [k+m][B][L]: every unit column is one contiguous region
             st = torch.empty((k + m, e - b, L), dtype=torch.uint8, device=dev).transpose(0, 1)
         else:                      # [B][k+m][L]: stripes back to back
             st = torch.empty((e - b, k + m, L), dtype=torch.uint8, device=dev)
@@ -303,7 +313,8 @@ def config_mixed(args, world, rank, dev):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic", "verified": ok, "classes": per_class,
-            "config": {"layout": "[k+m][B][L] unit-major" if args.layout == "unit" else "[B][k+m][L] stripe-major",
+            "config": {"layout": {f"{L}B": "[k+m][B][L] unit-major" if layout_for(args, L) == "unit"
+                                  else "[B][k+m][L] stripe-major" for L, _, _ in classes},
                        "workload": "RS(6,4) encode+decode (erase 0), 1 GiB data per class "
                                    "(1 KiB x 262144, 4 KiB x 65536, 1 MiB x 256 stripes) over all ranks",
                        "parallelism": f"per-class byte-balanced stripe partition x{world}"}}
@@ -669,7 +680,7 @@ def main():
     n = k + m
     coder = RSCoder(k, m)
     g = torch.Generator(device=dev).manual_seed(0xE1EC7 + rank)
-    if args.layout == "unit":  # [k+m][B][L] layout experiment
+    if layout_for(args, L) == "unit":  # [k+m][B][L] layout experiment
         stripe = torch.empty((n, B, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L].transpose(0, 1)
     else:
         stripe = torch.empty((B, n, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L]
