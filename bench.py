@@ -12,6 +12,9 @@ slowest rank's time, in GiB/s.  roofline = the encode kernel (dominant launch):
 algorithmic bytes (k+m)*L*B per launch / its mean HIP-event duration, against
 the 8.0 TB/s HBM3E peak.  cpu_baseline = the oracle's ISA-L-algorithm SIMD path
 on the host cores, rank 0 only (test infrastructure, not the product path).
+sizes = the same step and timing at the north star's other chunk sizes (1 KiB,
+1 MiB; 1 GiB of data per rank each) next to the 64 KiB line, so every
+--gpus N run reports all three.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--chunk BYTES] [--stripes B]
   multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
@@ -57,6 +60,8 @@ def parse():
                     help="target CPU-baseline work time (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (PCIe) measurement")
+    ap.add_argument("--no-sizes", action="store_true",
+                    help="headline: skip the 1 KiB / 1 MiB chunk-size lines (sizes) after the 64 KiB one")
     ap.add_argument("--config", default="headline",
                     choices=["headline", "mixed", "rs12", "hostpath", "update", "padded", "hashed", "flows"],
                     help="headline = the driver's line (BASELINE configs[1]+[2]); mixed = configs[3] "
@@ -222,6 +227,49 @@ def decode_sweep(coder, stripe, k, m, L, B, stream, reps=5):
         gbs = B * (k + 1) * L / (ms * 1e-3) / 1e9
         res[f"erase{j}"] = {"ms": round(ms, 4), "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                             "verified": bool(torch.equal(out[:, 0], stripe[:, j]))}
+    return res
+
+
+def size_sweep(args, world, rank, dev, coder, sizes=(1024, 1 << 20)):
+    """The north star's other chunk sizes (1 KiB and 1 MiB next to the headline's
+    64 KiB), each timed exactly like the headline after it: the same step
+    (encode + single-erasure decode) over 1 GiB of data per rank, barrier +
+    synchronize on both sides, max over ranks, value = all ranks' data / time.
+    Layout per the policy of layout_for().  Per-kernel fractions from HIP events
+    on this rank."""
+    from elect_amd.batch import decode_batch, encode_batch
+    k, m = coder.k, coder.m
+    res = {}
+    for L in sizes:
+        B = (1 << 30) // (k * L)
+        if layout_for(args, L) == "unit":
+            st = torch.empty((k + m, B, L), dtype=torch.uint8, device=dev).transpose(0, 1)
+        else:
+            st = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
+        st[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev)
+        out = torch.empty((B, 1, L), dtype=torch.uint8, device=dev)
+        evs = []
+
+        def step():
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record()
+            encode_batch(coder, st[:, :k], st[:, k:])
+            e[1].record()
+            decode_batch(coder, st, list(range(1, k + 1)), [0], out, inputs_by_unit=True)
+            e[2].record()
+            evs.append(e)
+
+        dt = timed(step, args.steps, args.warmup, world)
+        enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs[-args.steps:]) / args.steps
+        dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs[-args.steps:]) / args.steps
+        res[str(L)] = {
+            "value": round(world * args.steps * 2 * B * k * L / dt / GIB, 2), "unit": "GiB/s",
+            "ms_per_step": round(dt / args.steps * 1e3, 4), "stripes_per_gpu": B,
+            "layout": "[k+m][B][L]" if layout_for(args, L) == "unit" else "[B][k+m][L]",
+            "encode_frac": round(B * (k + m) * L / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "decode_frac": round(B * (k + 1) * L / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "verified": bool(torch.equal(out[:, 0], st[:, 0]))}
+        del st, out
     return res
 
 
@@ -774,6 +822,15 @@ def main():
         },
         "verified": ok,
     }
+    if not args.no_sizes:  # every rank: the sweep has its own barriers and max over ranks
+        out["sizes"] = size_sweep(args, world, rank, dev, coder)
+        out["sizes"][str(L)] = {"value": out["value"], "unit": "GiB/s", "ms_per_step": out["ms_per_step"],
+                                "stripes_per_gpu": B, "layout": "[B][k+m][L]" if layout_for(args, L) == "stripe"
+                                else "[k+m][B][L]", "encode_frac": out["kernels"]["encode"]["frac"],
+                                "decode_frac": out["kernels"]["decode_1erasure"]["frac"], "verified": ok}
+        out["sizes"] = {key: out["sizes"][key] for key in sorted(out["sizes"], key=int)}
+        ok = ok and all(v["verified"] for v in out["sizes"].values())
+        out["verified"] = ok
     if rank == 0:
         out["kernels"]["decode_sweep"] = sw = decode_sweep(coder, stripe, k, m, L, B, stream)
         ok = ok and all(v["verified"] for v in sw.values())

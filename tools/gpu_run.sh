@@ -28,12 +28,12 @@ for step in "$@"; do
     bench) run bench 600 python bench.py || exit $? ;;
     prof)
         run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run \
-            -- python3 bench.py --no-cpu --no-host --steps 50 --warmup 5 || exit $? ;;
+            -- python3 bench.py --no-cpu --no-host --no-sizes --steps 50 --warmup 5 || exit $? ;;
     pmc)
         run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_$TAG -o run \
-            -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $?
+            -- python3 bench.py --no-cpu --no-host --no-sizes --steps 5 --warmup 1 || exit $?
         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run \
-            -- python3 bench.py --no-cpu --no-host --steps 5 --warmup 1 || exit $? ;;
+            -- python3 bench.py --no-cpu --no-host --no-sizes --steps 5 --warmup 1 || exit $? ;;
     profcfg)  # rocprof kernel stats of one bench config: PROF_CFG="--config hashed ..."
         run profcfg 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profcfg_$TAG -o run \
             -- python3 bench.py ${PROF_CFG:-} --no-cpu --no-host --steps 20 --warmup 3 || exit $? ;;
