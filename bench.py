@@ -638,19 +638,23 @@ def config_flows(args, world, rank, dev):
     coder = RSCoder(k, m)
     g = torch.Generator(device=dev)
     g.manual_seed(0xE1EC7)
-    stripe = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
+    # units at a 256-byte pitch (a codeLength like 4,404,020 B, = 4 mod 16, would
+    # otherwise put every unit start off 16-byte alignment)
+    pitch = (L + 255) & ~255
+    stripe = torch.empty((B, k + m, pitch), dtype=torch.uint8, device=dev)[:, :, :L]
     data, par = stripe[:, :k], stripe[:, k:]
     data.copy_(torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g))
     top = int(L / 1.05)
     lens = torch.randint(int(top * 0.95), top + 1, (B, k), dtype=torch.int32, device=dev, generator=g)
-    new = torch.randint(0, 256, (B, L), dtype=torch.uint8, device=dev, generator=g)
+    new = torch.empty((B, pitch), dtype=torch.uint8, device=dev)[:, :L]
+    new.copy_(torch.randint(0, 256, (B, L), dtype=torch.uint8, device=dev, generator=g))
     t = 1
     ulens = torch.stack([lens[:, t], torch.randint(int(top * 0.95), top + 1, (B,), dtype=torch.int32, device=dev,
                                                    generator=g)], dim=1).contiguous()
     surv = [j for j in range(k) if j != t] + [k]  # degraded read of unit t from the others + parity 0
     dlens = torch.cat([lens[:, [j for j in range(k) if j != t]],
                        torch.full((B, 1), L, dtype=torch.int32, device=dev)], dim=1).contiguous()
-    rebuilt = torch.empty((B, 1, L), dtype=torch.uint8, device=dev)
+    rebuilt = torch.empty((B, 1, pitch), dtype=torch.uint8, device=dev)[:, :, :L]
     h_enc = torch.empty((B, m), dtype=torch.int32, device=dev)
     h_upd = torch.empty((B, m), dtype=torch.int32, device=dev)
     ev = {"encode": [], "update": [], "decode": []}
@@ -703,7 +707,8 @@ def config_flows(args, world, rank, dev):
                          "algorithmic_bytes_per_launch": alg["encode"],
                          "fill": round(valid / (B * k * L), 3)},
             "config": {"workload": f"{B} stripes x {L} B codeLength per GPU; encode all, update unit {t} in place, "
-                                   f"rebuild unit {t} from units {surv}", "parallelism": f"stripe-partitioned x{world}"}}
+                                   f"rebuild unit {t} from units {surv}", "layout": f"[B][k+m][{pitch}] (unit pitch "
+                                   "rounded up to 256 B)", "parallelism": f"stripe-partitioned x{world}"}}
 
 
 def main():
