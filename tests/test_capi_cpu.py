@@ -147,7 +147,7 @@ def test_no_device_fails_loudly():
 
 
 def test_flow_entry_points_validate_before_device_work():
-    """encode_ex / encode_update_ex: argument errors and the no-op cases need no device."""
+    """encode_ex / encode_update_ex / decode_ex: argument errors and the no-op cases need no device."""
     from elect_amd import _lib
     from elect_amd.coder import RSCoder
     c = RSCoder(4, 2)
@@ -162,7 +162,16 @@ def test_flow_entry_points_validate_before_device_work():
     # hashCode() of an empty buffer is 1 (no device work)
     assert c.encode_ex_host(ins[:4], outs, 0, hashed=True) == [1, 1]
     assert c.encode_update_ex_host(ins, 0, outs, 0, hashed=True) == [1, 1]
+    out = [p[0].ctypes.data]
+    with pytest.raises(_lib.ECInvalidArgument):  # more erasures than m (JEC/CoderUtil.java:79-82)
+        c.decode_ex_host(ins[1:5], [1, 2, 3, 4], [0, 5, 1], out * 3, 64, input_lengths=[64] * 4)
+    with pytest.raises(_lib.ECInvalidArgument):  # survivor index out of range
+        c.decode_ex_host(ins[1:5], [1, 2, 3, 9], [0], out, 64, input_lengths=[64] * 4)
+    # a zero-length decode is a no-op before any device work (JEC/ErasureDecoder.java:36-38)
+    assert c.decode_ex_host(ins[1:5], [1, 2, 3, 4], [0], out, 0, input_lengths=[5, 0, 0, 7]) == 0
     if not gpu_available():
+        with pytest.raises(_lib.ECDeviceError):
+            c.decode_ex_host(ins[1:5], [1, 2, 3, 4], [0], out, 64, input_lengths=[64, 10, 0, 64])
         with pytest.raises(_lib.ECDeviceError):
             c.encode_ex_host(ins[:4], outs, 64, data_lengths=[64, 3, 0, 64], hashed=True)
         with pytest.raises(_lib.ECDeviceError):
