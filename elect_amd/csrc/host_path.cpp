@@ -42,6 +42,7 @@ public:
             if (pin_out_[s]) (void)hipHostFree(pin_out_[s]);
             if (d_in_[s]) (void)hipFree(d_in_[s]);
             if (d_out_[s]) (void)hipFree(d_out_[s]);
+            if (d_scratch_[s]) (void)hipFree(d_scratch_[s]);
         }
         if (d_hash_) (void)hipFree(d_hash_);
     }
@@ -126,6 +127,8 @@ private:
             p.hashes = d_hash_;
             p.hash_stride = static_cast<uint32_t>(op.rows);
             p.hash_base = offset;
+            p.hash_scratch = d_scratch_[s];  // per slot: the two slots' launches overlap
+            p.hash_scratch_words = kScratchWords;
         }
         return kern::launch_apply(p, stream_[s]);
     }
@@ -137,7 +140,9 @@ private:
                 const hipError_t e = hipStreamCreateWithFlags(&stream_[s], hipStreamNonBlocking);
                 if (e != hipSuccess) return map_hip(e);
             }
-            const hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_hash_), kern::kMaxRows * sizeof(int32_t));
+            hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_hash_), kern::kMaxRows * sizeof(int32_t));
+            for (int s = 0; s < kSlots && e == hipSuccess; ++s)
+                e = hipMalloc(reinterpret_cast<void**>(&d_scratch_[s]), kScratchWords * sizeof(uint32_t));
             if (e != hipSuccess) return map_hip(e);
         }
         if (in_bytes > cap_in_) {
@@ -182,6 +187,11 @@ private:
     size_t cap_in_ = 0;
     size_t cap_out_ = 0;
     int32_t* d_hash_ = nullptr;
+    // Hash partials of one slot's launch.  Engine-owned rather than taken from the
+    // stream-ordered pool per launch: with many caller threads, each on its own
+    // streams, pool-allocated partials were corrupted (host_stress).
+    static constexpr size_t kScratchWords = kern::hash_scratch_need(kChunk / 16);
+    uint32_t* d_scratch_[kSlots] = {};
 };
 
 constexpr int kMaxDevices = 64;
@@ -374,6 +384,8 @@ private:
         uint8_t *pin_in = nullptr, *pin_out = nullptr, *d_in = nullptr, *d_out = nullptr;
         uint32_t *pin_lens = nullptr, *d_lens = nullptr;  // [slot][cols]
         int32_t *pin_hash = nullptr, *d_hash = nullptr;    // [slot][rows]
+        uint32_t* d_scratch = nullptr;                       // hash partials of the batch's launch
+        size_t scratch_words = 0;
         std::condition_variable done;  // this batch's callers wait here for kDone
         hipStream_t stream = nullptr;
         hipEvent_t h2d_done = nullptr;
@@ -422,6 +434,8 @@ private:
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_lens), meta);
             if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_hash), meta, hipHostMallocDefault);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_hash), meta);
+            s.scratch_words = kern::hash_scratch_need(arena / 16);  // a batch has at most arena/16 segments
+            if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_scratch), s.scratch_words * sizeof(uint32_t));
             if (e != hipSuccess) return map_hip(e);
         }
         return ELECT_EC_OK;
@@ -493,6 +507,8 @@ private:
                 p.hashes = s.d_hash;
                 p.hash_stride = static_cast<uint32_t>(s.rows);
                 p.hash_seed = true;
+                p.hash_scratch = s.d_scratch;
+                p.hash_scratch_words = s.scratch_words;
             }
             e = kern::launch_apply(p, s.stream);
         }

@@ -600,7 +600,10 @@ __global__ __launch_bounds__(kBlock) void hash_reduce(const uint32_t* __restrict
     sum = wave_sum(sum);
     if (lane == 0) {
         uint32_t* h = reinterpret_cast<uint32_t*>(hashes) + static_cast<uint64_t>(s) * hstride + r;
-        *h = (hi ? seed : *h) + sum;
+        if (hi)
+            *h = seed + sum;
+        else  // add mode: launches over other windows of the same units may add concurrently (host path)
+            atomicAdd(h, sum);
     }
 }
 
@@ -615,6 +618,92 @@ inline int block_for(uint64_t len, int coefs) { return (len <= 4096 || coefs >= 
 #endif
 
 constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches are encodes
+
+// Hash-partial scratch when the caller brings none (the device-resident API):
+// one buffer per (device, stream), reused only in that stream's order, grown or
+// handed to another stream only after an event recorded behind its last use.
+// Stream-ordered allocation (hipMallocAsync / hipFreeAsync, default or private
+// pool) corrupted partials when many threads launched on their own streams:
+// freed blocks were handed out again while a reduce still read them
+// (tools/sanitize/host_stress; a never-freed hipMalloc variant was clean).
+struct ScratchEntry {
+    std::mutex mu;           // held from lease to release: launches on one stream serialise
+    hipStream_t stream = nullptr;
+    bool assigned = false;
+    uint64_t last = 0;       // LRU tick (under the cache mutex)
+    uint32_t* ptr = nullptr;
+    size_t words = 0;
+    hipEvent_t done = nullptr;  // recorded behind the last launch that used ptr
+    hipStream_t done_on = nullptr;
+    bool recorded = false;
+};
+
+struct ScratchCache {
+    std::mutex mu;
+    uint64_t tick = 0;
+    ScratchEntry e[16];
+};
+
+ScratchCache g_scratch[64];
+
+// Returns with entry->mu held; scratch_release() records the event and unlocks.
+hipError_t scratch_lease(hipStream_t stream, size_t words, ScratchEntry** out)
+{
+    int dev = 0;
+    hipError_t err = hipGetDevice(&dev);
+    if (err != hipSuccess) return err;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    ScratchCache& c = g_scratch[dev];
+    for (;;) {
+        ScratchEntry* e = nullptr;
+        {
+            std::lock_guard<std::mutex> lock(c.mu);
+            for (ScratchEntry& x : c.e)
+                if (x.assigned && x.stream == stream) e = &x;
+            if (!e) {  // a free entry, else the least recently used one
+                for (ScratchEntry& x : c.e)
+                    if (!e || (!x.assigned && e->assigned) || (x.assigned == e->assigned && x.last < e->last)) e = &x;
+                e->assigned = true;
+                e->stream = stream;
+            }
+            e->last = ++c.tick;
+        }
+        e->mu.lock();
+        if (!e->assigned || e->stream != stream) {  // taken over for another stream meanwhile
+            e->mu.unlock();
+            continue;
+        }
+        if (e->recorded && e->done_on != stream) {  // last used on another stream: wait for it
+            err = hipEventSynchronize(e->done);
+            e->recorded = err != hipSuccess;
+        }
+        if (err == hipSuccess && e->words < words) {
+            if (e->recorded) err = hipEventSynchronize(e->done);  // its last use on this stream
+            e->recorded = false;
+            if (err == hipSuccess && e->ptr) err = hipFree(e->ptr);
+            e->ptr = nullptr;
+            e->words = 0;
+            if (err == hipSuccess) err = hipMalloc(reinterpret_cast<void**>(&e->ptr), words * sizeof(uint32_t));
+            if (err == hipSuccess) e->words = words;
+        }
+        if (err == hipSuccess && !e->done) err = hipEventCreateWithFlags(&e->done, hipEventDisableTiming);
+        if (err != hipSuccess) {
+            e->mu.unlock();
+            return err;
+        }
+        *out = e;
+        return hipSuccess;
+    }
+}
+
+hipError_t scratch_release(ScratchEntry* e, hipStream_t stream)
+{
+    const hipError_t err = hipEventRecord(e->done, stream);
+    e->recorded = err == hipSuccess;
+    e->done_on = stream;
+    e->mu.unlock();
+    return err;
+}
 
 template <int K, int R, bool PAD>
 hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
@@ -655,11 +744,10 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         a.total = static_cast<uint32_t>(ns * segs64);
         a.hpart = nullptr;
         a.hpart_hi = nullptr;
-        if (a.hashes) {  // stream-ordered scratch for the per-wave partial sums (lo, then hi)
+        if (a.hashes) {  // the per-wave partial sums (lo, then hi) go to the caller's scratch
             const size_t n = (static_cast<size_t>(a.total) / 64 + 1) * R;
-            const hipError_t e =
-                hipMallocAsync(reinterpret_cast<void**>(&a.hpart), (hash_assign ? 2 : 1) * n * sizeof(uint32_t), stream);
-            if (e != hipSuccess) return e;
+            if (!p.hash_scratch || 2 * n > p.hash_scratch_words) return hipErrorInvalidValue;
+            a.hpart = p.hash_scratch;
             if (hash_assign) a.hpart_hi = a.hpart + n;
         }
         bool lens_path = false;
@@ -689,10 +777,6 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             hipLaunchKernelGGL(hash_reduce, dim3((n + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, stream, a.hpart,
                                a.hpart_hi, a.hashes, a.hstride, R, a.segs, static_cast<uint32_t>(ns), pow31(p.len));
             e = hipGetLastError();
-        }
-        if (a.hpart) {
-            const hipError_t f = hipFreeAsync(a.hpart, stream);
-            if (e == hipSuccess) e = f;
         }
         if (e != hipSuccess) return e;
     }
@@ -1008,7 +1092,7 @@ bool apply_is_aligned(const ApplyParams& p)
     return true;
 }
 
-hipError_t launch_apply(const ApplyParams& p_in, hipStream_t stream)
+hipError_t launch_apply_impl(const ApplyParams& p_in, hipStream_t stream)
 {
     if (p_in.cols < 1 || p_in.cols > kMaxCols || p_in.rows < 1 || p_in.rows > kMaxRows) return hipErrorInvalidValue;
     if (p_in.stripes == 0) return hipSuccess;
@@ -1047,6 +1131,24 @@ hipError_t launch_apply(const ApplyParams& p_in, hipStream_t stream)
         if (e != hipSuccess) return e;
     }
     return (p.len & 15) ? launch_bytes(tail_of(p), stream) : hipSuccess;
+}
+
+hipError_t launch_apply(const ApplyParams& p_in, hipStream_t stream)
+{
+    if (!p_in.hashes || p_in.hash_scratch || p_in.len == 0 || p_in.stripes == 0)
+        return launch_apply_impl(p_in, stream);
+    // hashed, no caller scratch: the stream's cached buffer (scratch_lease)
+    const uint64_t segs = p_in.padded ? (p_in.len + 15) / 16 : p_in.len / 16;
+    const uint64_t total = std::min<uint64_t>(segs * p_in.stripes, kMaxIndex);
+    ScratchEntry* e = nullptr;
+    hipError_t err = scratch_lease(stream, hash_scratch_need(total), &e);
+    if (err != hipSuccess) return err;
+    ApplyParams p = p_in;
+    p.hash_scratch = e->ptr;
+    p.hash_scratch_words = e->words;
+    err = launch_apply_impl(p, stream);
+    const hipError_t r = scratch_release(e, stream);
+    return err != hipSuccess ? err : r;
 }
 
 hipError_t launch_update(const UpdateParams& p, hipStream_t stream)

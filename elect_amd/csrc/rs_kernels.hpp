@@ -66,6 +66,11 @@ struct ApplyParams {
     // and assigned by hash_reduce with no memset and no atomics; otherwise the
     // launcher seeds the entries (hipMemsetD32Async) and the kernels add.
     bool hash_seed = false;
+    // Optional caller-owned device scratch for the per-wave hash partials
+    // (hash_scratch_need() words, used in the caller's stream order); without
+    // it launch_apply leases the stream's cached buffer.
+    uint32_t* hash_scratch = nullptr;
+    size_t hash_scratch_words = 0;
     // internal (launch_apply): every column start is 16-byte aligned.  When it
     // is not, the dwordx4 kernels still run (unaligned vector access, see
     // unaligned_vector_ok) except gf_apply_lens, whose buffer loads need it.
@@ -95,6 +100,10 @@ struct UpdateParams {
 };
 
 hipError_t launch_apply(const ApplyParams& p, hipStream_t stream);
+
+// Scratch words a hashed launch_apply over `segments` 16-byte segments in all
+// (stripes x ceil(len/16)) needs at most (row groups run one after another).
+constexpr size_t hash_scratch_need(uint64_t segments) { return (segments / 64 + 1) * kFastRows * 2; }
 hipError_t launch_update(const UpdateParams& p, hipStream_t stream);
 
 // True when every column start is 16-byte aligned for every stripe.

@@ -364,3 +364,51 @@ def test_device_lengths_above_chunk_count_as_full(dev, oracle):
         dl = np.concatenate([lens[:, 1:], np.full((B, 1), -1, np.int32)], axis=1)  # survivors 1, 2, 3, P0
         decode_batch_ex(RSCoder(k, m), stripe, [1, 2, 3, 4], [0], out, lengths=_to(dev, dl), inputs_by_unit=True)
         assert torch.equal(out[:, 0], d_data[:, 0])  # unit 0's lengths are all above L: full
+
+
+def test_concurrent_streams_hashed_device_api(dev, oracle):
+    """Many threads, each launching hashed encodes on its own stream (the device API
+    leases a per-stream scratch for the hash partials).  Stream-ordered pool scratch
+    (hipMallocAsync / hipFreeAsync) corrupted partials in exactly this pattern
+    (tools/sanitize/host_stress); every hash must still match the JDK loop."""
+    import threading
+    from elect_amd.batch import encode_batch_ex
+    from elect_amd.coder import RSCoder
+    k, m = 4, 2
+    coder = RSCoder(k, m)
+    enc = oracle.Encoder(k, m)
+    errors = []
+
+    def worker(t):
+        try:
+            torch.cuda.set_device(dev)
+            s = torch.cuda.Stream()
+            rng = np.random.default_rng(700 + t)
+            for it in range(6):
+                B, L = int(rng.integers(1, 5)), int(rng.choice([1500, 4099, 20000, 65536 + 4]))
+                data = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+                lens = rng.integers(0, L + 1, size=(B, k)).astype(np.int32)
+                with torch.cuda.stream(s):
+                    d = torch.from_numpy(data).to(dev, non_blocking=False)
+                    dl = torch.from_numpy(lens).to(dev)
+                    par = torch.empty((B, m, L), dtype=torch.uint8, device=dev)
+                    hs = torch.empty((B, m), dtype=torch.int32, device=dev)
+                    encode_batch_ex(coder, d, par, lengths=dl, hashes=hs, stream=s)
+                s.synchronize()
+                got_p, got_h = par.cpu().numpy(), hs.cpu().numpy()
+                for b in range(B):
+                    want = enc.encode([oracle.zero_fill(data[b, j, :lens[b, j]], L) for j in range(k)])
+                    for r in range(m):
+                        if not np.array_equal(got_p[b, r], want[r]):
+                            errors.append(f"t{t} it{it} parity {b} {r}")
+                        if int(got_h[b, r]) != oracle.java_hashcode(want[r]):
+                            errors.append(f"t{t} it{it} hash {b} {r} L={L}")
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:5]

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Build the engine's HOST code with AddressSanitizer + UndefinedBehaviorSanitizer
+# (device code is not instrumented: GPU sanitizers are unavailable on this pool)
+# and run the concurrency stress driver.  Build here (no GPU needed), run on the box:
+#   tools/sanitize/run.sh build     -> tools/sanitize/out/{libelect_ec_san.so,host_stress}
+#   tools/sanitize/run.sh run [T] [N]
+set -eu
+cd "$(dirname "$0")/../.."
+OUT=tools/sanitize/out
+H=/opt/rocm/bin/hipcc
+SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer"
+case "${1:-build}" in
+build)
+    mkdir -p $OUT
+    for f in ec_capi.cpp host_path.cpp rs_kernels.hip; do
+        $H --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -I include $SAN -x hip -c elect_amd/csrc/$f -o $OUT/${f%.*}.o &
+    done
+    wait
+    $H --offload-arch=gfx950 -shared -fPIC $SAN -o $OUT/libelect_ec_san.so $OUT/ec_capi.o $OUT/host_path.o $OUT/rs_kernels.o
+    $H --offload-arch=gfx950 -O1 -g -std=c++17 -I include $SAN -x hip tools/sanitize/host_stress.cpp -o $OUT/host_stress \
+        -L $OUT -lelect_ec_san -Wl,-rpath,'$ORIGIN' -pthread
+    rm -f $OUT/*.o
+    echo built $OUT/host_stress ;;
+run)
+    # the pool's harness preloads a library of its own, so ASan cannot come first in the link order
+    ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0:halt_on_error=1:abort_on_error=0 \
+    UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 \
+        $OUT/host_stress "${2:-24}" "${3:-12}" "${4:-1}" ;;
+esac
