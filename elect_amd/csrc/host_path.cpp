@@ -338,7 +338,7 @@ public:
         if (slot == 0 || slab->full) cv_worker_.notify_one();
         lock.unlock();
 
-        const size_t in_stride = static_cast<size_t>(slab->cols) * pitch;
+        const size_t in_stride = static_cast<size_t>(op.cols) * pitch;  // == the slab's (matches())
         if (op.lens) {  // only the content bytes; the kernel reads the rest as zero
             for (int j = 0; j < op.cols; ++j) {
                 slab->pin_lens[static_cast<size_t>(slot) * op.cols + j] = static_cast<uint32_t>(op.lens[j]);
@@ -355,7 +355,7 @@ public:
         lock.unlock();
 
         if (status == ELECT_EC_OK) {
-            const size_t out_stride = static_cast<size_t>(slab->rows) * pitch;
+            const size_t out_stride = static_cast<size_t>(op.rows) * pitch;
             for (int r = 0; r < op.rows; ++r)
                 std::memcpy(op.out[r], slab->pin_out + slot * out_stride + r * pitch, len);
             if (op.hashes)
@@ -370,6 +370,13 @@ public:
     }
 
 private:
+    struct Shape {  // what a batch computes, copied out of its slab under mu_
+        int cols = 0, rows = 0;
+        size_t len = 0, pitch = 0;
+        bool padded = false, hashed = false;
+        uint8_t coef[kern::kMaxRows * kern::kMaxCols] = {};
+    };
+
     struct Slab {
         enum State { kFree, kOpen, kInFlight, kDone } state = kFree;
         Batcher* owner = nullptr;
@@ -389,6 +396,19 @@ private:
         std::condition_variable done;  // this batch's callers wait here for kDone
         hipStream_t stream = nullptr;
         hipEvent_t h2d_done = nullptr;
+
+        Shape shape() const
+        {
+            Shape sh;
+            sh.cols = cols;
+            sh.rows = rows;
+            sh.len = len;
+            sh.pitch = pitch;
+            sh.padded = padded;
+            sh.hashed = hashed;
+            std::memcpy(sh.coef, coef, sizeof(coef));
+            return sh;
+        }
 
         bool matches(const HostOp& op, size_t n) const
         {
@@ -471,9 +491,10 @@ private:
             s->full = true;
             s->state = Slab::kInFlight;  // no more reservations
             cv_worker_.wait(lock, [&] { return s->filled == s->reserved; });
+            const Shape shape = s->shape();  // under mu_: open() rewrites these for the slab's next batch
             const int n = s->reserved;
             lock.unlock();
-            const hipError_t e = issue(*s, n);
+            const hipError_t e = issue(*s, shape, n);
             if (e != hipSuccess) (void)hipStreamSynchronize(s->stream);  // no callback was queued
             lock.lock();
             if (e != hipSuccess) finish(s, map_hip(e));
@@ -481,31 +502,33 @@ private:
         }
     }
 
-    static hipError_t issue(Slab& s, int n)
+    // s's buffers, stream and event never change after init(); its shape is
+    // read from the copy taken under mu_.
+    static hipError_t issue(Slab& s, const Shape& sh, int n)
     {
-        const size_t in_stride = static_cast<size_t>(s.cols) * s.pitch;
-        const size_t out_stride = static_cast<size_t>(s.rows) * s.pitch;
+        const size_t in_stride = static_cast<size_t>(sh.cols) * sh.pitch;
+        const size_t out_stride = static_cast<size_t>(sh.rows) * sh.pitch;
         hipError_t e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
-        if (e == hipSuccess && s.padded)
-            e = hipMemcpyAsync(s.d_lens, s.pin_lens, static_cast<size_t>(n) * s.cols * sizeof(uint32_t),
+        if (e == hipSuccess && sh.padded)
+            e = hipMemcpyAsync(s.d_lens, s.pin_lens, static_cast<size_t>(n) * sh.cols * sizeof(uint32_t),
                                hipMemcpyHostToDevice, s.stream);
         if (e == hipSuccess) e = hipEventRecord(s.h2d_done, s.stream);
         if (e == hipSuccess) {
             ApplyParams p;
-            p.len = s.len;
+            p.len = sh.len;
             p.stripes = static_cast<uint64_t>(n);
-            p.cols = s.cols;
-            p.rows = s.rows;
-            for (int j = 0; j < s.cols; ++j) p.src[j] = col(s.d_in, in_stride, j * s.pitch);
-            for (int r = 0; r < s.rows; ++r) p.dst[r] = col(s.d_out, out_stride, r * s.pitch);
-            std::memcpy(p.coef, s.coef, sizeof(p.coef));
-            if (s.padded) {
+            p.cols = sh.cols;
+            p.rows = sh.rows;
+            for (int j = 0; j < sh.cols; ++j) p.src[j] = col(s.d_in, in_stride, j * sh.pitch);
+            for (int r = 0; r < sh.rows; ++r) p.dst[r] = col(s.d_out, out_stride, r * sh.pitch);
+            std::memcpy(p.coef, sh.coef, sizeof(p.coef));
+            if (sh.padded) {
                 p.padded = true;
                 p.lens = s.d_lens;
             }
-            if (s.hashed) {
+            if (sh.hashed) {
                 p.hashes = s.d_hash;
-                p.hash_stride = static_cast<uint32_t>(s.rows);
+                p.hash_stride = static_cast<uint32_t>(sh.rows);
                 p.hash_seed = true;
                 p.hash_scratch = s.d_scratch;
                 p.hash_scratch_words = s.scratch_words;
@@ -513,8 +536,8 @@ private:
             e = kern::launch_apply(p, s.stream);
         }
         if (e == hipSuccess) e = hipMemcpyAsync(s.pin_out, s.d_out, n * out_stride, hipMemcpyDeviceToHost, s.stream);
-        if (e == hipSuccess && s.hashed)
-            e = hipMemcpyAsync(s.pin_hash, s.d_hash, static_cast<size_t>(n) * s.rows * sizeof(int32_t),
+        if (e == hipSuccess && sh.hashed)
+            e = hipMemcpyAsync(s.pin_hash, s.d_hash, static_cast<size_t>(n) * sh.rows * sizeof(int32_t),
                                hipMemcpyDeviceToHost, s.stream);
         if (e == hipSuccess) e = hipLaunchHostFunc(s.stream, &Batcher::on_done, &s);
         return e;

@@ -4,11 +4,17 @@
 # and run the concurrency stress driver.  Build here (no GPU needed), run on the box:
 #   tools/sanitize/run.sh build     -> tools/sanitize/out/{libelect_ec_san.so,host_stress}
 #   tools/sanitize/run.sh run [T] [N]
+#   SANITIZER=tsan tools/sanitize/run.sh build|run   (ThreadSanitizer instead)
 set -eu
 cd "$(dirname "$0")/../.."
 OUT=tools/sanitize/out
 H=/opt/rocm/bin/hipcc
-SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer"
+if [ "${SANITIZER:-asan}" = tsan ]; then  # ThreadSanitizer build: tools/sanitize/out_tsan
+    SAN="-Xarch_host -fsanitize=thread -Xarch_host -fno-omit-frame-pointer"
+    OUT=tools/sanitize/out_tsan
+else
+    SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer"
+fi
 case "${1:-build}" in
 build)
     mkdir -p $OUT
@@ -25,5 +31,6 @@ run)
     # the pool's harness preloads a library of its own, so ASan cannot come first in the link order
     ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0:halt_on_error=1:abort_on_error=0 \
     UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 \
+    TSAN_OPTIONS=report_signal_unsafe=0:second_deadlock_stack=1 \
         $OUT/host_stress "${2:-24}" "${3:-12}" "${4:-1}" ;;
 esac
