@@ -112,33 +112,6 @@ __device__ __forceinline__ void store_nt(uint8_t* p, const uint4& v)
     __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
 }
 
-// Output stores of the fast kernels: non-temporal, or plain when the launch
-// writes at most a quarter of what it reads (4R <= K: decodes with e = 1 of
-// k = 4, e = 2 of k = 8).  Plain stores write-combine in L2 and measured
-// +4 points on those shapes even back to back (64 KiB RS(6,4) decode 78.6 ->
-// 82.9 % of peak, the encode+decode step +1.9 %); on encodes (R/K = 1/2) they
-// cost 7-15 points.  A compile-time choice: with a runtime flag the compiler
-// merged the two stores into one plain store, dropping the nt hint everywhere.
-// AB_STORE (A/B builds): 1 nt always, 2 plain always.
-#ifndef AB_STORE
-#define AB_STORE 0
-#endif
-template <int K, int R>
-constexpr bool plain_stores()
-{
-    return AB_STORE ? AB_STORE == 2 : 4 * R <= K;
-}
-
-template <bool PLAIN>
-__device__ __forceinline__ void store_out(uint8_t* p, const uint4& v)
-{
-    if constexpr (PLAIN) {
-        *reinterpret_cast<uint4*>(p) = v;
-    } else {
-        store_nt(p, v);
-    }
-}
-
 // Partial segments (padded launches only): n < 16 valid bytes, zero filled.
 __device__ __forceinline__ uint4 load_partial(const uint8_t* p, uint32_t n)
 {
@@ -435,7 +408,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
     gf_combine<K, R>(x, tl, acc);
     if (!PAD || off + 16 <= a.len) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) store_out<plain_stores<K, R>()>(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
+        for (int r = 0; r < R; ++r) store_nt(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
     } else {
         const uint32_t n = static_cast<uint32_t>(a.len - off);
 #pragma unroll
@@ -564,7 +537,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
             uint4 acc[R];
             gf_combine<K, R, true>(x[u], tl, acc, cmask);
 #pragma unroll
-            for (int r = 0; r < R; ++r) store_out<plain_stores<K, R>()>(a.dp[r] + s0 * a.ds[r] + off, acc[r]);
+            for (int r = 0; r < R; ++r) store_nt(a.dp[r] + s0 * a.ds[r] + off, acc[r]);
         }
         return;
     }
@@ -589,7 +562,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
         uint4 acc[R];
         gf_combine<K, R>(x, tl, acc);
 #pragma unroll
-        for (int r = 0; r < R; ++r) store_out<plain_stores<K, R>()>(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
+        for (int r = 0; r < R; ++r) store_nt(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
     }
 }
 
