@@ -52,6 +52,10 @@ def parse():
                          "6 KiB region), stripe-major above")
     ap.add_argument("--decode-out", choices=("separate", "inplace"), default="separate",
                     help="headline decode target: a separate [B][1][L] buffer, or the erased unit's own slot")
+    ap.add_argument("--rotate", type=int, default=4,
+                    help="headline and sizes: cycle through N disjoint stripe batches (1 GiB of data each), "
+                         "one per step, so that no step finds the previous one's lines in L2 or the 256 MiB "
+                         "MALL (DESIGN.md §5)")
     ap.add_argument("--rebuilt-rows", type=int, default=1,
                     help="layout experiment: the separate decode buffer is [B][rows][L], row 0 used")
     ap.add_argument("--unit-gap", type=int, default=0,
@@ -242,15 +246,18 @@ def size_sweep(args, world, rank, dev, coder, sizes=(1024, 1 << 20)):
     res = {}
     for L in sizes:
         B = (1 << 30) // (k * L)
-        if layout_for(args, L) == "unit":
-            st = torch.empty((k + m, B, L), dtype=torch.uint8, device=dev).transpose(0, 1)
-        else:
-            st = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
-        st[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev)
-        out = torch.empty((B, 1, L), dtype=torch.uint8, device=dev)
+        sets = []  # --rotate: disjoint batches in turn, as in the headline
+        for _ in range(args.rotate):
+            if layout_for(args, L) == "unit":
+                st = torch.empty((k + m, B, L), dtype=torch.uint8, device=dev).transpose(0, 1)
+            else:
+                st = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
+            st[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev)
+            sets.append((st, torch.empty((B, 1, L), dtype=torch.uint8, device=dev)))
         evs = []
 
         def step():
+            st, out = sets[len(evs) % len(sets)]
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             e[0].record()
             encode_batch(coder, st[:, :k], st[:, k:])
@@ -268,8 +275,8 @@ def size_sweep(args, world, rank, dev, coder, sizes=(1024, 1 << 20)):
             "layout": "[k+m][B][L]" if layout_for(args, L) == "unit" else "[B][k+m][L]",
             "encode_frac": round(B * (k + m) * L / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "decode_frac": round(B * (k + 1) * L / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "verified": bool(torch.equal(out[:, 0], st[:, 0]))}
-        del st, out
+            "verified": all(bool(torch.equal(out[:, 0], st[:, 0])) for st, out in sets)}
+        del sets
     return res
 
 
@@ -733,17 +740,23 @@ def main():
     n = k + m
     coder = RSCoder(k, m)
     g = torch.Generator(device=dev).manual_seed(0xE1EC7 + rank)
-    if layout_for(args, L) == "unit":  # [k+m][B][L] layout experiment
-        stripe = torch.empty((n, B, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L].transpose(0, 1)
-    else:
-        stripe = torch.empty((B, n, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L]
-    stripe[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g)
-    rebuilt = torch.empty((B, args.rebuilt_rows, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :1, :L]
+    sets = []  # --rotate N: N disjoint stripe batches, one per step in turn (no cache reuse across steps)
+    for _ in range(args.rotate):
+        if layout_for(args, L) == "unit":  # [k+m][B][L] layout experiment
+            st = torch.empty((n, B, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L].transpose(0, 1)
+        else:
+            st = torch.empty((B, n, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L]
+        st[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g)
+        sets.append((st, torch.empty((B, args.rebuilt_rows, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :1, :L]))
+    stripe, rebuilt = sets[0]
+    turn = [0]
     survivors = list(range(1, k + 1))
     stream = torch.cuda.current_stream()
     orig0 = stripe[:, 0].clone() if args.decode_out == "inplace" else None
 
     def step(ev=None):
+        stripe, rebuilt = sets[turn[0] % len(sets)]
+        turn[0] += 1
         if ev is not None:
             ev[0].record(stream)
         encode_batch(coder, stripe[:, :k], stripe[:, k:], stream=stream)
@@ -776,7 +789,7 @@ def main():
     if args.decode_out == "inplace":  # unit 0 was rebuilt in place: it must still be the original data
         ok = bool(torch.equal(stripe[:, 0], orig0))
     else:
-        ok = bool(torch.equal(rebuilt[:, 0], stripe[:, 0]))
+        ok = all(bool(torch.equal(r[:, 0], st[:, 0])) for st, r in sets)
 
     data_bytes_per_rank_step = 2 * B * k * L  # encode k*L + decode k*L survivors, per stripe
     value = world * args.steps * data_bytes_per_rank_step / elapsed / GIB
@@ -804,6 +817,7 @@ def main():
                         f"{survivors}), {B} stripes x {L} B chunks per GPU "
                         f"({B * k * L / GIB:.2f} GiB data per op per GPU)",
             "k": k, "m": m, "chunk_bytes": L, "stripes_per_gpu": B,
+            "rotate": args.rotate,  # disjoint batches per rank, one per step in turn
             "parallelism": f"stripe-partitioned x{world}, no collectives",
         },
         "roofline": {
