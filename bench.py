@@ -46,7 +46,9 @@ def parse():
     ap.add_argument("--m", type=int, default=2)
     ap.add_argument("--chunk", type=int, default=65536)
     ap.add_argument("--stripes", type=int, default=4096)
-    ap.add_argument("--layout", choices=("auto", "stripe", "unit"), default="auto",
+    ap.add_argument("--no-tiles", action="store_true",
+                    help="layout auto: stripe-major instead of 64 KiB tiles for chunks above 64 KiB")
+    ap.add_argument("--layout", choices=("auto", "stripe", "unit", "tiled"), default="auto",
                     help="HBM layout of the stripes ([B][k+m][L] or [k+m][B][L]); headline and mixed. auto: "
                          "unit-major for chunks <= 4 KiB (a stripe-major wave would read and write one "
                          "6 KiB region), stripe-major above")
@@ -248,12 +250,8 @@ def size_sweep(args, world, rank, dev, coder, sizes=(1024, 1 << 20)):
         B = (1 << 30) // (k * L)
         sets = []  # --rotate: disjoint batches in turn, as in the headline
         for _ in range(args.rotate):
-            if layout_for(args, L) == "unit":
-                st = torch.empty((k + m, B, L), dtype=torch.uint8, device=dev).transpose(0, 1)
-            else:
-                st = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
-            st[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev)
-            sets.append((st, torch.empty((B, 1, L), dtype=torch.uint8, device=dev)))
+            st, Bc, Lc = alloc_stripes(args, B, L, k, m, dev)
+            sets.append((st, torch.empty((Bc, 1, Lc), dtype=torch.uint8, device=dev)))
         evs = []
 
         def step():
@@ -272,7 +270,7 @@ def size_sweep(args, world, rank, dev, coder, sizes=(1024, 1 << 20)):
         res[str(L)] = {
             "value": round(world * args.steps * 2 * B * k * L / dt / GIB, 2), "unit": "GiB/s",
             "ms_per_step": round(dt / args.steps * 1e3, 4), "stripes_per_gpu": B,
-            "layout": "[k+m][B][L]" if layout_for(args, L) == "unit" else "[B][k+m][L]",
+            "layout": LAYOUT_NAMES[layout_for(args, L)],
             "encode_frac": round(B * (k + m) * L / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "decode_frac": round(B * (k + 1) * L / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "verified": all(bool(torch.equal(out[:, 0], st[:, 0])) for st, out in sets)}
@@ -297,12 +295,42 @@ def device_copy_rate(dev, nbytes=1 << 30, reps=5):
     return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
 
 
+TILE = 1 << 16  # the unit size HBM streams best back to back
+LAYOUT_NAMES = {"unit": "[k+m][B][L]", "stripe": "[B][k+m][L]", "tiled": "[B][L/64K][k+m][64K]"}
+
+
 def layout_for(args, L: int) -> str:
     """HBM layout of a batch of L-byte chunks: --layout, or for "auto" unit-major
-    [k+m][B][L] when L <= 4 KiB and stripe-major [B][k+m][L] above."""
+    [k+m][B][L] when L <= 4 KiB, stripe-major [B][k+m][L] up to 64 KiB, and for
+    larger multiples of 64 KiB 64 KiB tiles [B][L/64K][k+m][64K]."""
     if args.layout != "auto":
         return args.layout
-    return "unit" if L <= 4096 else "stripe"
+    if L <= 4096:
+        return "unit"
+    return "tiled" if L > TILE and L % TILE == 0 and not args.no_tiles else "stripe"
+
+
+def alloc_stripes(args, B: int, L: int, k: int, m: int, dev, generator=None):
+    """A batch of B stripes of k+m L-byte units in the layout of layout_for(),
+    data units filled with random bytes.  Returns the coding view (Bc, k+m, Lc)
+    and Bc, Lc.  Tiled: each stripe is stored as L/64K tiles of k+m 64 KiB
+    units and coded as B*L/64K stripes of 64 KiB; RS works bytewise, so every
+    chunk's parity is the same bytes as coding it whole."""
+    layout = layout_for(args, L)
+    if layout == "tiled":
+        if L % TILE:
+            raise ValueError("--layout tiled needs chunks that are a multiple of 64 KiB")
+        t = L // TILE
+        st = torch.empty((B, t, k + m, TILE), dtype=torch.uint8, device=dev).view(B * t, k + m, TILE)
+        Bc, Lc = B * t, TILE
+    elif layout == "unit":
+        st = torch.empty((k + m, B, L), dtype=torch.uint8, device=dev).transpose(0, 1)
+        Bc, Lc = B, L
+    else:
+        st = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
+        Bc, Lc = B, L
+    st[:, :k] = torch.randint(0, 256, (Bc, k, Lc), dtype=torch.uint8, device=dev, generator=generator)
+    return st, Bc, Lc
 
 
 def timed(step, steps, warmup, world):
@@ -331,12 +359,8 @@ def config_mixed(args, world, rank, dev):
     for L in (1024, 4096, 1 << 20):
         total = (1 << 30) // (k * L)
         b, e = partition_by_bytes([k * L] * total, world, rank)
-        if layout_for(args, L) == "unit":  # [k+m][B][L]: every unit column is one contiguous region
-            st = torch.empty((k + m, e - b, L), dtype=torch.uint8, device=dev).transpose(0, 1)
-        else:                      # [B][k+m][L]: stripes back to back
-            st = torch.empty((e - b, k + m, L), dtype=torch.uint8, device=dev)
-        st[:, :k] = torch.randint(0, 256, (e - b, k, L), dtype=torch.uint8, device=dev)
-        classes.append((L, st, torch.empty((e - b, 1, L), dtype=torch.uint8, device=dev)))
+        st, Bc, Lc = alloc_stripes(args, e - b, L, k, m, dev)
+        classes.append((L, st, torch.empty((Bc, 1, Lc), dtype=torch.uint8, device=dev)))
 
     def step():
         for L, st, out in classes:
@@ -359,17 +383,16 @@ def config_mixed(args, world, rank, dev):
             torch.cuda.synchronize()
             t["encode"].append(ev[0].elapsed_time(ev[1]))
             t["decode"].append(ev[1].elapsed_time(ev[2]))
-        B = st.shape[0]
+        B, Lc = st.shape[0], st.shape[2]  # the coding view (tiled: B*L/64K stripes of 64 KiB)
         enc_ms, dec_ms = sorted(t["encode"])[4], sorted(t["decode"])[4]
-        per_class[f"{L}B"] = {"encode_frac": round(B * (k + m) * L / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                              "decode_frac": round(B * (k + 1) * L / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        per_class[f"{L}B"] = {"encode_frac": round(B * (k + m) * Lc / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "decode_frac": round(B * (k + 1) * Lc / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     return {"metric": "GiB/s device-resident RS(6,4) encode+decode, mixed 1 KiB/4 KiB/1 MiB chunks",
             "value": round(args.steps * data / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic", "verified": ok, "classes": per_class,
-            "config": {"layout": {f"{L}B": "[k+m][B][L] unit-major" if layout_for(args, L) == "unit"
-                                  else "[B][k+m][L] stripe-major" for L, _, _ in classes},
+            "config": {"layout": {f"{L}B": LAYOUT_NAMES[layout_for(args, L)] for L, _, _ in classes},
                        "workload": "RS(6,4) encode+decode (erase 0), 1 GiB data per class "
                                    "(1 KiB x 262144, 4 KiB x 65536, 1 MiB x 256 stripes) over all ranks",
                        "parallelism": f"per-class byte-balanced stripe partition x{world}"}}
@@ -742,10 +765,16 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0xE1EC7 + rank)
     sets = []  # --rotate N: N disjoint stripe batches, one per step in turn (no cache reuse across steps)
     for _ in range(args.rotate):
+        if args.unit_gap == 0 and args.rebuilt_rows == 1:
+            st, Bc, Lc = alloc_stripes(args, B, L, k, m, dev, generator=g)
+            sets.append((st, torch.empty((Bc, 1, Lc), dtype=torch.uint8, device=dev)))
+            continue
         if layout_for(args, L) == "unit":  # [k+m][B][L] layout experiment
             st = torch.empty((n, B, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L].transpose(0, 1)
-        else:
+        elif layout_for(args, L) == "stripe":
             st = torch.empty((B, n, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :, :L]
+        else:
+            raise ValueError("--unit-gap / --rebuilt-rows experiments take the unit or stripe layout")
         st[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g)
         sets.append((st, torch.empty((B, args.rebuilt_rows, L + args.unit_gap), dtype=torch.uint8, device=dev)[:, :1, :L]))
     stripe, rebuilt = sets[0]
@@ -844,8 +873,7 @@ def main():
     if not args.no_sizes:  # every rank: the sweep has its own barriers and max over ranks
         out["sizes"] = size_sweep(args, world, rank, dev, coder)
         out["sizes"][str(L)] = {"value": out["value"], "unit": "GiB/s", "ms_per_step": out["ms_per_step"],
-                                "stripes_per_gpu": B, "layout": "[B][k+m][L]" if layout_for(args, L) == "stripe"
-                                else "[k+m][B][L]", "encode_frac": out["kernels"]["encode"]["frac"],
+                                "stripes_per_gpu": B, "layout": LAYOUT_NAMES[layout_for(args, L)], "encode_frac": out["kernels"]["encode"]["frac"],
                                 "decode_frac": out["kernels"]["decode_1erasure"]["frac"], "verified": ok}
         out["sizes"] = {key: out["sizes"][key] for key in sorted(out["sizes"], key=int)}
         ok = ok and all(v["verified"] for v in out["sizes"].values())

@@ -579,3 +579,26 @@ def test_cross_thread_batching(dev, oracle):
     finally:
         _lib.set_batching(True)  # the library default
     assert not errors, errors[:5]
+
+
+def test_tiled_layout_equals_contiguous(dev):
+    """bench.py's layout for chunks above 64 KiB ([B][L/64K][k+m][64K], coded as
+    B*L/64K stripes of 64 KiB): every chunk's parity and rebuilt
+    unit are the same bytes as coding the chunk whole in [B][k+m][L]."""
+    from elect_amd.batch import decode_batch, encode_batch
+    from elect_amd.coder import RSCoder
+    k, m, B, L, T = 4, 2, 3, 1 << 20, 1 << 16
+    coder = RSCoder(k, m)
+    g = torch.Generator(device=dev).manual_seed(31)
+    flat = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
+    flat[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g)
+    tiled = torch.empty((B, L // T, k + m, T), dtype=torch.uint8, device=dev)
+    tiled[:, :, :k] = flat[:, :k].reshape(B, k, L // T, T).transpose(1, 2)
+    view = tiled.view(B * (L // T), k + m, T)
+    encode_batch(coder, flat[:, :k], flat[:, k:])
+    encode_batch(coder, view[:, :k], view[:, k:])
+    out = torch.empty((B * (L // T), 1, T), dtype=torch.uint8, device=dev)
+    decode_batch(coder, view, [1, 2, 3, 4], [0], out, inputs_by_unit=True)
+    torch.cuda.synchronize()
+    assert torch.equal(tiled[:, :, k:].transpose(1, 2).reshape(B, m, L), flat[:, k:])
+    assert torch.equal(out.view(B, L), flat[:, 0])

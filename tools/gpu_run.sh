@@ -99,6 +99,12 @@ for step in "$@"; do
                 ELECT_EC_LIB=$lib run "ab_${v}_${tag}_$i" 300 python bench.py --config $cfg $extra $args --no-cpu --no-host --steps 50 || exit $?
             done
         done; done ;;
+    tiles)  # 64 KiB tiles for chunks above 64 KiB (layout auto) against stripe-major, interleaved
+        for i in 1 2 3; do for v in "" "--no-tiles"; do
+            tag=${v:-tiles}; tag=${tag//-/}
+            run "bench_tiles_${tag}_headline_$i" 300 python bench.py --no-cpu --no-host $v || exit $?
+            run "bench_tiles_${tag}_mixed_$i" 300 python bench.py --config mixed $v || exit $?
+        done; done ;;
     padfill)  # padded encode vs content fill: where the time goes
         for f in 1.0 0.0 0.5 random; do
             run "bench_padded_fill_$f" 300 python bench.py --config padded --pad-fill $f || exit $?
