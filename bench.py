@@ -405,10 +405,9 @@ def config_rs12(args, world, rank, dev):
     from elect_amd.coder import RSCoder
     k, m, L, B = 8, 4, 262144, 512
     coder = RSCoder(k, m)
-    st = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
-    st[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev)
+    st, Bc, Lc = alloc_stripes(args, B, L, k, m, dev)  # layout policy of layout_for (64 KiB tiles)
     encode_batch(coder, st[:, :k], st[:, k:])
-    out = torch.empty((B, 2, L), dtype=torch.uint8, device=dev)
+    out = torch.empty((Bc, 2, Lc), dtype=torch.uint8, device=dev)
     surv = list(range(2, 10))
     evs = []
 
@@ -450,6 +449,7 @@ def config_rs12(args, world, rank, dev):
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                          "kernel": "gf_apply_x16<8,2> (decode)", "algorithmic_bytes_per_launch": alg},
             "config": {"workload": f"RS(12,8) decode erase {{0,1}} from {surv}, {B} x {L} B stripes per GPU",
+                       "layout": LAYOUT_NAMES[layout_for(args, L)],
                        "parallelism": f"stripe-partitioned x{world}"}}
 
 

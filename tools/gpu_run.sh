@@ -104,6 +104,7 @@ for step in "$@"; do
             tag=${v:-tiles}; tag=${tag//-/}
             run "bench_tiles_${tag}_headline_$i" 300 python bench.py --no-cpu --no-host $v || exit $?
             run "bench_tiles_${tag}_mixed_$i" 300 python bench.py --config mixed $v || exit $?
+            run "bench_tiles_${tag}_rs12_$i" 300 python bench.py --config rs12 $v || exit $?
         done; done ;;
     padfill)  # padded encode vs content fill: where the time goes
         for f in 1.0 0.0 0.5 random; do
