@@ -279,10 +279,69 @@ constexpr int kTabStride = 8;  // dwords per coefficient in LDS
 
 // cmask (wave-uniform): columns to include; the others are known zero for the
 // whole wave and are skipped by a scalar branch (padded launches).
+// Unmasked launches take columns in pairs: the six lookups of a pair fold into
+// the accumulator with three XOR3s (v_bitop3), 9 VALU ops per pair, row and
+// dword against 10 one column at a time (RS(12,8) encode: -48 of 887 per wave).
+template <int K, int R>
+__device__ __forceinline__ void gf_combine_pairs(const uint4 (&x)[K], const uint32_t* tl, uint4 (&acc)[R])
+{
+#pragma unroll
+    for (int j = 0; j < K; j += 2) {
+        constexpr int kPair = 2;
+        const bool two = j + 1 < K;
+        uint32_t s0[kPair][4], s1[kPair][4], s2[kPair][4];
+#pragma unroll
+        for (int c = 0; c < kPair; ++c)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const Sel sl = selectors(lane_word(x[(c == 0 || !two) ? j : j + 1], w));
+                s0[c][w] = sl.s0;
+                s1[c][w] = sl.s1;
+                s2[c][w] = sl.s2;
+            }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t* ta = &tl[(r * K + j) * kTabStride];
+            const uint4 qa = *reinterpret_cast<const uint4*>(ta);
+            const uint32_t a2 = ta[4];
+            uint4 qb = qa;
+            uint32_t b2 = a2;
+            if (two) {
+                const uint32_t* tb = &tl[(r * K + j + 1) * kTabStride];
+                qb = *reinterpret_cast<const uint4*>(tb);
+                b2 = tb[4];
+            }
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t p0 = __builtin_amdgcn_perm(qa.y, qa.x, s0[0][w]);
+                const uint32_t p1 = __builtin_amdgcn_perm(qa.w, qa.z, s1[0][w]);
+                const uint32_t p2 = __builtin_amdgcn_perm(a2, a2, s2[0][w]);
+                uint32_t v;
+                if (!two) {  // odd K: the last column alone
+                    v = j == 0 ? xor3(p0, p1, p2) : (xor3(lane_word(acc[r], w), p0, p1) ^ p2);
+                } else {
+                    const uint32_t q0 = __builtin_amdgcn_perm(qb.y, qb.x, s0[1][w]);
+                    const uint32_t q1 = __builtin_amdgcn_perm(qb.w, qb.z, s1[1][w]);
+                    const uint32_t q2 = __builtin_amdgcn_perm(b2, b2, s2[1][w]);
+                    v = j == 0 ? (xor3(xor3(p0, p1, p2), q0, q1) ^ q2)
+                               : xor3(xor3(xor3(lane_word(acc[r], w), p0, p1), p2, q0), q1, q2);
+                }
+                set_word(acc[r], w, v);
+            }
+        }
+    }
+}
+
 template <int K, int R, bool MASKED = false>
 __device__ __forceinline__ void gf_combine(const uint4 (&x)[K], const uint32_t* tl, uint4 (&acc)[R],
                                            uint32_t cmask = ~0u)
 {
+#ifndef AB_COMBINE1
+    if constexpr (!MASKED) {
+        gf_combine_pairs<K, R>(x, tl, acc);
+        return;
+    }
+#endif
     if (MASKED) {
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
