@@ -17,7 +17,11 @@ sizes = the same step and timing at the north star's other chunk sizes (1 KiB,
 --gpus N run reports all three.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--chunk BYTES] [--stripes B]
-  multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+
+With --gpus N > 1 and no launcher in the environment (no WORLD_SIZE), bench.py
+starts N rank processes itself under torch.distributed.run; under a launcher
+it refuses to run unless WORLD_SIZE == N.  Ranks talk only over gloo (barrier,
+max over ranks, per-rank records); no RCCL communicator is created.
 """
 from __future__ import annotations
 
@@ -83,12 +87,37 @@ def parse():
     ap.add_argument("--host-op", choices=("encode", "encode_ex"), default="encode",
                     help="hostpath: plain encode (the JNI encodeImpl), or ELECT's fused encode step "
                          "(encodeExImpl: content = codeLength/1.05, parity hashCodes)")
+    ap.add_argument("--graph", action="store_true",
+                    help="headline and mixed: capture each step's launches in a HIP graph and replay it")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="plumbing check without a GPU: start the ranks, run the gloo handshake, print "
+                         "one JSON line (tests/test_bench_launch_cpu.py)")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` started without a launcher: run N rank processes under
+    torch.distributed.run (rendezvous on 127.0.0.1) as a child and return its exit
+    status.  This process never touches the GPU, so nothing exec's from a process
+    that has initialised HIP."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__), *argv]
+    return subprocess.run(cmd).returncode
 
 
 def dist_setup(args):
     from elect_amd import dist
-    return dist.setup("cuda")
+    return dist.setup("cpu" if args.launch_check else "cuda")
 
 
 def barrier(world):
@@ -115,15 +144,46 @@ def pmc_traffic(kernel_substr: str):
     return None, None
 
 
-def cpu_baseline(args, k, m, L):
-    """Oracle SIMD path (ISA-L's algorithm restated) on the host cores; bounded sample."""
+def host_cpu_info() -> dict:
+    """The host cores this process may use: affinity mask, cgroup CPU quota, model."""
+    info = {"affinity": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(), "quota_cores": None,
+            "model": None}
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+            if path.endswith("cpu.max") and parts[0] != "max":
+                info["quota_cores"] = round(int(parts[0]) / int(parts[1]), 2)
+            elif path.endswith("quota_us") and int(parts[0]) > 0:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    info["quota_cores"] = round(int(parts[0]) / int(f.read()), 2)
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return info
+
+
+def cpu_baseline(args, k, m, L, stripes):
+    """Oracle SIMD path (ISA-L's algorithm restated) on the host cores: the same
+    encode + single-erasure decode step over the same stripe batch the GPU codes
+    (4096 x 64 KiB: 1 GiB of data, 1.75 GiB touched, far beyond any LLC), one
+    thread per CPU in the affinity mask, stripes split evenly over them; then the
+    same loop on one thread.  Bounded to about --cpu-seconds of threaded work."""
     import numpy as np
     from oracle import ec_oracle as orc
-    threads = max(1, min(16, os.cpu_count() or 1))
-    stripes = 250  # BASELINE configs[0]: 1000 data chunks of 64 KiB
+    info = host_cpu_info()
+    threads = info["affinity"]
     n = k + m
-    rng = np.random.default_rng(0xE1EC7)
-    buf = rng.integers(0, 256, size=(stripes, n, L), dtype=np.uint8)
+    buf = np.empty((stripes, n, L), np.uint8)
+    orc.fill_splitmix(0xE1EC7, buf)
     em = orc.cauchy_matrix(k, m)
     enc_coef = em[k:]
     rc, dec_coef = orc.decode_matrix(k, m, list(range(1, k + 1)), [0])
@@ -133,32 +193,34 @@ def cpu_baseline(args, k, m, L):
     enc_src = [j * L for j in range(k)]
     enc_dst = [(k + r) * L for r in range(m)]
     dec_src = [j * L for j in range(1, k + 1)]
-    # warm, then repeat encode+decode until the time budget is used
-    orc.batch_apply(enc_coef, buf, sstride, enc_src, buf, sstride, enc_dst, L, stripes, threads, level)
-    total_t, reps = 0.0, 0
-    while total_t < args.cpu_seconds or reps < 2:
-        total_t += orc.batch_apply(enc_coef, buf, sstride, enc_src, buf, sstride, enc_dst, L, stripes,
-                                   threads, level)
-        total_t += orc.batch_apply(dec_coef, buf, sstride, dec_src, out, L, [0], L, stripes, threads, level)
-        reps += 1
+
+    def loop(nthreads, budget, min_reps):
+        t, reps = 0.0, 0
+        while t < budget or reps < min_reps:
+            t += orc.batch_apply(enc_coef, buf, sstride, enc_src, buf, sstride, enc_dst, L, stripes, nthreads, level)
+            t += orc.batch_apply(dec_coef, buf, sstride, dec_src, out, L, [0], L, stripes, nthreads, level)
+            reps += 1
+        return reps, t
+
+    orc.batch_apply(enc_coef, buf, sstride, enc_src, buf, sstride, enc_dst, L, stripes, threads, level)  # warm
+    reps, total_t = loop(threads, args.cpu_seconds, 2)
     assert np.array_equal(out[:, 0], buf[:, 0]), "CPU baseline decode mismatch"
-    data_bytes = 2 * reps * stripes * k * L
-    # single-core figure: the same loop on one thread, ~3 s
-    t1, reps1 = 0.0, 0
-    while t1 < args.cpu_seconds * 0.3 or reps1 < 1:
-        t1 += orc.batch_apply(enc_coef, buf, sstride, enc_src, buf, sstride, enc_dst, L, stripes, 1, level)
-        t1 += orc.batch_apply(dec_coef, buf, sstride, dec_src, out, L, [0], L, stripes, 1, level)
-        reps1 += 1
+    reps1, t1 = loop(1, args.cpu_seconds * 0.3, 1)  # single-core figure
+    step_bytes = 2 * stripes * k * L
     return {
-        "single_core_GiB/s": round(2 * reps1 * stripes * k * L / t1 / GIB, 3),
-        "value": round(data_bytes / total_t / GIB, 3),
+        "value": round(reps * step_bytes / total_t / GIB, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"RS({n},{k}) encode+decode (erase 0), {stripes} stripes x {L} B "
-                  f"({stripes * k} data chunks), {reps} reps, {total_t:.1f} s, "
-                  f"oracle {orc.simd_name(level)} x {threads} threads",
-    }, buf
+        "single_core_GiB/s": round(reps1 * step_bytes / t1 / GIB, 3),
+        "working_set_bytes": int(buf.nbytes + out.nbytes),
+        "cpu_model": info["model"],
+        "affinity_cpus": info["affinity"],
+        "cgroup_quota_cores": info["quota_cores"],
+        "sample": f"RS({n},{k}) encode + decode (erase 0) of the GPU's batch: {stripes} stripes x {L} B "
+                  f"({stripes * k * L / GIB:.2f} GiB data), {reps} reps in {total_t:.1f} s on {threads} threads; "
+                  f"{reps1} reps in {t1:.1f} s on 1; oracle {orc.simd_name(level)} (ISA-L's algorithm)",
+    }
 
 
 def host_inclusive(coder, k, m, L, stripes_total, dev):
@@ -264,12 +326,13 @@ def size_sweep(args, world, rank, dev, coder, sizes=(1024, 1 << 20)):
             e[2].record()
             evs.append(e)
 
-        dt = timed(step, args.steps, args.warmup, world)
+        dt, submit = timed(step, args.steps, args.warmup, world)
         enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs[-args.steps:]) / args.steps
         dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs[-args.steps:]) / args.steps
         res[str(L)] = {
             "value": round(world * args.steps * 2 * B * k * L / dt / GIB, 2), "unit": "GiB/s",
             "ms_per_step": round(dt / args.steps * 1e3, 4), "stripes_per_gpu": B,
+            "host_submit_ms_per_step": round(submit, 4),
             "layout": LAYOUT_NAMES[layout_for(args, L)],
             "encode_frac": round(B * (k + m) * L / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "decode_frac": round(B * (k + 1) * L / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -334,17 +397,46 @@ def alloc_stripes(args, B: int, L: int, k: int, m: int, dev, generator=None):
 
 
 def timed(step, steps, warmup, world):
+    """Warm up, then time exactly `steps` steps between barrier + synchronize on
+    both sides.  Returns (max over ranks of the elapsed seconds, this rank's host
+    submit time per step in ms: the time the host spends issuing one step's
+    launches, which must stay well below the step's GPU time)."""
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
+    submit = 0.0
     t0 = time.perf_counter()
     for _ in range(steps):
+        s0 = time.perf_counter()
         step()
+        submit += time.perf_counter() - s0
     torch.cuda.synchronize()
     barrier(world)
-    return max_over_ranks(time.perf_counter() - t0, world)
+    return max_over_ranks(time.perf_counter() - t0, world), submit / steps * 1e3
+
+
+def graph_steps(fns):
+    """Capture each of fns (one step's launches each) in its own HIP graph on a
+    side stream; returns their replay functions.  The launchers only enqueue
+    kernels on the current stream (no host sync, no allocation once warm), so the
+    captured graph replays exactly the launches an eager step makes."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    graphs = []
+    with torch.cuda.stream(side):
+        for fn in fns:
+            fn()  # warm: one-time device probes and table uploads happen outside the capture
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    for fn in fns:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        graphs.append(g)
+    torch.cuda.synchronize()
+    return [g.replay for g in graphs]
 
 
 def config_mixed(args, world, rank, dev):
@@ -367,7 +459,8 @@ def config_mixed(args, world, rank, dev):
             encode_batch(coder, st[:, :k], st[:, k:])
             decode_batch(coder, st, [1, 2, 3, 4], [0], out, inputs_by_unit=True)
 
-    dt = timed(step, args.steps, args.warmup, world)
+    run = graph_steps([step])[0] if args.graph else step
+    dt, submit = timed(run, args.steps, args.warmup, world)
     ok = all(torch.equal(out[:, 0], st[:, 0]) for _, st, out in classes)
     data = 2 * 3 * (1 << 30)  # enc + dec, 3 classes, all ranks together
     per_class = {}  # outside the timed region: each class's kernels by HIP events (median of 9)
@@ -390,6 +483,7 @@ def config_mixed(args, world, rank, dev):
     return {"metric": "GiB/s device-resident RS(6,4) encode+decode, mixed 1 KiB/4 KiB/1 MiB chunks",
             "value": round(args.steps * data / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "host_submit_ms_per_step": round(submit, 4), "graph": bool(args.graph),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic", "verified": ok, "classes": per_class,
             "config": {"layout": {f"{L}B": LAYOUT_NAMES[layout_for(args, L)] for L, _, _ in classes},
@@ -418,7 +512,7 @@ def config_rs12(args, world, rank, dev):
         e1.record()
         evs.append((e0, e1))
 
-    dt = timed(step, args.steps, args.warmup, world)
+    dt, submit = timed(step, args.steps, args.warmup, world)
     ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
     ok = torch.equal(out, st[:, :2])
     alg = B * (k + 2) * L
@@ -443,7 +537,8 @@ def config_rs12(args, world, rank, dev):
                                    "frac": round(enc_gbs / HBM_PEAK_GBS, 4)}},
             "value": round(world * args.steps * B * k * L / dt / GIB, 2), "unit": "GiB/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(dt / args.steps * 1e3, 4), "host_submit_ms_per_step": round(submit, 4),
+            "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
@@ -542,7 +637,7 @@ def config_update(args, world, rank, dev):
         e1.record()
         evs.append((e0, e1))
 
-    dt = timed(step, args.steps, args.warmup, world)
+    dt, submit = timed(step, args.steps, args.warmup, world)
     ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
     # self-check through the product: updating twice with the same delta restores the parity
     ref = par.clone()
@@ -585,7 +680,7 @@ def config_padded(args, world, rank, dev):
         e1.record()
         evs.append((e0, e1))
 
-    dt = timed(step, args.steps, args.warmup, world)
+    dt, submit = timed(step, args.steps, args.warmup, world)
     ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
     # self-check through the product: explicit zero fill + plain encode gives the same parity
     idx = torch.arange(L, device=dev).view(1, 1, L)
@@ -630,7 +725,7 @@ def config_hashed(args, world, rank, dev):
         e1.record()
         evs.append((e0, e1))
 
-    dt = timed(step, args.steps, args.warmup, world)
+    dt, submit = timed(step, args.steps, args.warmup, world)
     ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
     ref = torch.empty_like(par)
     encode_batch(coder, data, ref)
@@ -701,7 +796,7 @@ def config_flows(args, world, rank, dev):
         for i, n in enumerate(("encode", "update", "decode")):
             ev[n].append((es[i], es[i + 1]))
 
-    dt = timed(step, args.steps, args.warmup, world)
+    dt, submit = timed(step, args.steps, args.warmup, world)
     ms = {n: sum(a.elapsed_time(b) for a, b in v[-args.steps:]) / args.steps for n, v in ev.items()}
     # self-check through the product: the updated parity is the encode of the new zero-filled
     # stripe, its hashes match, and the degraded read returns the new unit zero filled
@@ -741,21 +836,60 @@ def config_flows(args, world, rank, dev):
                                    "rounded up to 256 B)", "parallelism": f"stripe-partitioned x{world}"}}
 
 
+def launch_check(args, world, rank):
+    """--launch-check: the multi-rank plumbing with no GPU work (CPU test)."""
+    barrier(world)
+    t = max_over_ranks(float(rank + 1), world)
+    recs = gather({"rank": rank, "world": world, "pid": os.getpid()}, world)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "max_over_ranks": t, "ranks": recs}), flush=True)
+
+
+def gather(obj, world):
+    from elect_amd import dist
+    return dist.gather(obj, world)
+
+
+def finish(out, rank, world, rec) -> None:
+    """Every rank's own record (verified, own time, host submit time) to rank 0,
+    which prints the line; exit non-zero on every rank if any rank failed."""
+    from elect_amd import dist
+    recs = gather(rec, world)
+    ok = all(r["verified"] for r in recs)
+    out["verified"] = ok
+    out["ranks"] = recs
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.teardown(world)
+    if not ok:
+        sys.exit(1)
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: start one rank per GPU (before anything touches the GPU here)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if int(env_world or 1) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}: refusing to report a wrong n_gpus",
+              file=sys.stderr)
+        sys.exit(2)
     world, rank, local = dist_setup(args)
+    if args.launch_check:
+        launch_check(args, world, rank)
+        from elect_amd import dist
+        dist.teardown(world)
+        return
+    dev = torch.device("cuda", local)
     if args.config != "headline":
-        dev = torch.device("cuda", local if world > 1 else 0)
         fn = {"mixed": config_mixed, "rs12": config_rs12, "hostpath": config_hostpath,
               "update": config_update, "padded": config_padded, "hashed": config_hashed,
               "flows": config_flows}[args.config]
         out = fn(args, world, rank, dev)
-        if rank == 0:
-            print(json.dumps(out), flush=True)
-        from elect_amd import dist
-        dist.teardown(world)
-        sys.exit(0 if out.get("verified", True) else 1)
-    dev = torch.device("cuda", local if world > 1 else 0)
+        finish(out, rank, world, {"rank": rank, "device": local, "verified": bool(out.get("verified", True)),
+                                  "host_submit_ms_per_step": out.get("host_submit_ms_per_step")})
+        return
     from elect_amd.batch import decode_batch, encode_batch
     from elect_amd.coder import RSCoder
 
@@ -783,19 +917,29 @@ def main():
     stream = torch.cuda.current_stream()
     orig0 = stripe[:, 0].clone() if args.decode_out == "inplace" else None
 
+    def encode_of(st):
+        return lambda: encode_batch(coder, st[:, :k], st[:, k:])
+
+    def decode_of(st, rb):
+        if args.decode_out == "inplace":  # rebuild unit 0 into its own slot of the stripe
+            return lambda: decode_batch(coder, st, survivors, [0], st, inputs_by_unit=True, outputs_by_unit=True)
+        return lambda: decode_batch(coder, st, survivors, [0], rb, inputs_by_unit=True)
+
+    ops = [(encode_of(st), decode_of(st, rb)) for st, rb in sets]
+    replays = graph_steps([lambda e=e, d=d: (e(), d()) for e, d in ops]) if args.graph else None
+
     def step(ev=None):
-        stripe, rebuilt = sets[turn[0] % len(sets)]
+        i = turn[0] % len(sets)
         turn[0] += 1
         if ev is not None:
             ev[0].record(stream)
-        encode_batch(coder, stripe[:, :k], stripe[:, k:], stream=stream)
-        if ev is not None:
-            ev[1].record(stream)
-        if args.decode_out == "inplace":  # rebuild unit 0 into its own slot of the stripe
-            decode_batch(coder, stripe, survivors, [0], stripe, inputs_by_unit=True, outputs_by_unit=True,
-                         stream=stream)
+        if replays is not None:  # one graph per batch: encode + decode
+            replays[i]()
         else:
-            decode_batch(coder, stripe, survivors, [0], rebuilt, inputs_by_unit=True, stream=stream)
+            ops[i][0]()
+            if ev is not None:
+                ev[1].record(stream)
+            ops[i][1]()
         if ev is not None:
             ev[2].record(stream)
 
@@ -805,14 +949,25 @@ def main():
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     barrier(world)
     torch.cuda.synchronize()
+    submit = 0.0
     t0 = time.perf_counter()
     for i in range(args.steps):
+        s0 = time.perf_counter()
         step(evs[i])
+        submit += time.perf_counter() - s0
     torch.cuda.synchronize()
     barrier(world)
-    elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(elapsed, world)
+    own = time.perf_counter() - t0
+    elapsed = max_over_ranks(own, world)
+    submit_ms = submit / args.steps * 1e3
 
+    if replays is not None:  # per-kernel split from an eager pass (a graph replay is one span)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        replays, keep = None, replays
+        for i in range(args.steps):
+            step(evs[i])
+        torch.cuda.synchronize()
+        replays = keep
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     if args.decode_out == "inplace":  # unit 0 was rebuilt in place: it must still be the original data
@@ -847,8 +1002,10 @@ def main():
                         f"({B * k * L / GIB:.2f} GiB data per op per GPU)",
             "k": k, "m": m, "chunk_bytes": L, "stripes_per_gpu": B,
             "rotate": args.rotate,  # disjoint batches per rank, one per step in turn
-            "parallelism": f"stripe-partitioned x{world}, no collectives",
+            "parallelism": f"stripe-partitioned x{world}, no collectives (gloo timing handshake only)",
+            "graph": bool(args.graph),
         },
+        "host_submit_ms_per_step": round(submit_ms, 4),
         "roofline": {
             "bound": "hbm",
             "achieved": round(enc_gbs, 1),
@@ -870,30 +1027,29 @@ def main():
         },
         "verified": ok,
     }
+    rec = {"rank": rank, "device": local, "ms_per_step": round(own / args.steps * 1e3, 4),
+           "host_submit_ms_per_step": round(submit_ms, 4), "encode_frac": out["kernels"]["encode"]["frac"],
+           "decode_frac": out["kernels"]["decode_1erasure"]["frac"], "verified": ok}
     if not args.no_sizes:  # every rank: the sweep has its own barriers and max over ranks
         out["sizes"] = size_sweep(args, world, rank, dev, coder)
         out["sizes"][str(L)] = {"value": out["value"], "unit": "GiB/s", "ms_per_step": out["ms_per_step"],
-                                "stripes_per_gpu": B, "layout": LAYOUT_NAMES[layout_for(args, L)], "encode_frac": out["kernels"]["encode"]["frac"],
+                                "stripes_per_gpu": B, "host_submit_ms_per_step": round(submit_ms, 4),
+                                "layout": LAYOUT_NAMES[layout_for(args, L)],
+                                "encode_frac": out["kernels"]["encode"]["frac"],
                                 "decode_frac": out["kernels"]["decode_1erasure"]["frac"], "verified": ok}
         out["sizes"] = {key: out["sizes"][key] for key in sorted(out["sizes"], key=int)}
-        ok = ok and all(v["verified"] for v in out["sizes"].values())
-        out["verified"] = ok
+        rec["sizes_verified"] = all(v["verified"] for v in out["sizes"].values())
+        rec["sizes_submit_ms"] = {key: v["host_submit_ms_per_step"] for key, v in out["sizes"].items()}
+        rec["verified"] = rec["verified"] and rec["sizes_verified"]
     if rank == 0:
         out["kernels"]["decode_sweep"] = sw = decode_sweep(coder, stripe, k, m, L, B, stream)
-        ok = ok and all(v["verified"] for v in sw.values())
-        out["verified"] = ok
+        rec["verified"] = rec["verified"] and all(v["verified"] for v in sw.values())
         out["roofline"]["device_copy_GB/s"] = device_copy_rate(dev)
     if rank == 0 and not args.no_host:
         out["host_inclusive_GiB/s"] = host_inclusive(coder, k, m, L, min(B, 4096), dev)
     if rank == 0 and world == 1 and not args.no_cpu:
-        cb, _ = cpu_baseline(args, k, m, L)
-        out["cpu_baseline"] = cb
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    from elect_amd import dist
-    dist.teardown(world)
-    if not ok:
-        sys.exit(1)
+        out["cpu_baseline"] = cpu_baseline(args, k, m, L, B)
+    finish(out, rank, world, rec)
 
 
 if __name__ == "__main__":

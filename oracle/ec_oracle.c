@@ -528,9 +528,11 @@ double oracle_batch_apply(int level, int threads, const unsigned char* coef, int
         threads = stripes ? (int)stripes : 1;
     pthread_t* tid = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
     batch_job* jobs = (batch_job*)calloc((size_t)threads, sizeof(batch_job));
-    if (!tid || !jobs) {
+    char* started = (char*)calloc((size_t)threads, 1);
+    if (!tid || !jobs || !started) {
         free(tid);
         free(jobs);
+        free(started);
         return -1.0;
     }
     double t0 = now_s();
@@ -541,15 +543,21 @@ double oracle_batch_apply(int level, int threads, const unsigned char* coef, int
         jb->s1 = stripes * (size_t)(t + 1) / (size_t)threads;
         jb->src = src; jb->src_stripe = src_stripe; jb->src_col_off = src_col_off;
         jb->dst = dst; jb->dst_stripe = dst_stripe; jb->dst_row_off = dst_row_off;
-        if (t + 1 < threads)
-            pthread_create(&tid[t], NULL, batch_worker, jb);
+        /* a thread that cannot be created (task limits) runs its share inline */
+        if (t + 1 < threads) {
+            started[t] = pthread_create(&tid[t], NULL, batch_worker, jb) == 0;
+            if (!started[t])
+                batch_worker(jb);
+        }
     }
     batch_worker(&jobs[threads - 1]);
     for (int t = 0; t + 1 < threads; t++)
-        pthread_join(tid[t], NULL);
+        if (started[t])
+            pthread_join(tid[t], NULL);
     double t1 = now_s();
     free(tid);
     free(jobs);
+    free(started);
     return t1 - t0;
 }
 

@@ -225,6 +225,12 @@ def splitmix_bytes(seed: int, n: int) -> np.ndarray:
     return out
 
 
+def fill_splitmix(seed: int, out: np.ndarray) -> None:
+    """Fill a contiguous uint8 array in place with the splitmix64 stream."""
+    assert out.dtype == np.uint8 and out.flags.c_contiguous
+    lib().oracle_fill_splitmix(ctypes.c_uint64(seed), _p(out.reshape(-1)), out.size)
+
+
 def java_hashcode(b) -> int:
     """java.nio.ByteBuffer.hashCode() of the bytes b (JDK loop; ECMessageVerbHandler.java:328)."""
     b = np.ascontiguousarray(b, np.uint8)

@@ -9,7 +9,7 @@ rm -f gpurun_out/*.log gpurun_out/status.txt  # no stale logs from an earlier ca
 export PYTHONUNBUFFERED=1
 export TMPDIR=/tmp
 OUT="$PWD/gpurun_out"
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
 run() {  # name seconds cmd...
     local name=$1 t=$2; shift 2
     echo "[$(date +%T)] start $name" | tee -a gpurun_out/status.txt
@@ -57,13 +57,20 @@ for step in "$@"; do
     streams) run streams 300 tools/tune/tune_apply streams || exit $? ;;
     unitstride) run unitstride 300 tools/tune/tune_apply unitstride || exit $? ;;
     unaligned) run unaligned 120 tools/tune/tune_apply unaligned || exit $? ;;
-    multirank)  # rehearse the N>1 flow: 2 ranks sharing the one GPU, gloo handshake
-        export ELECT_BENCH_BACKEND=gloo
-        run bench_rehearse_2rank 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-            --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu || exit $?
-        run bench_rehearse_2rank_mixed 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-            --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --config mixed --steps 10 || exit $?
-        unset ELECT_BENCH_BACKEND ;;
+    multirank)  # rehearse the N>1 flow: bare `bench.py --gpus 2`, 2 ranks sharing the one GPU, gloo handshake
+        export ELECT_BENCH_SHARE_GPU=1
+        run bench_rehearse_2rank 600 python bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu || exit $?
+        run bench_rehearse_2rank_mixed 600 python bench.py --gpus 2 --config mixed --steps 10 || exit $?
+        unset ELECT_BENCH_SHARE_GPU ;;
+    graph)  # host submit time: eager vs HIP-graph replay, headline and mixed
+        run bench_eager_nosizes 300 python bench.py --no-cpu --no-host --no-sizes --steps 50 || exit $?
+        run bench_graph 300 python bench.py --graph --no-cpu --no-host --no-sizes --steps 50 || exit $?
+        run bench_mixed_eager 300 python bench.py --config mixed --steps 20 || exit $?
+        run bench_mixed_graph 300 python bench.py --config mixed --graph --steps 20 || exit $? ;;
+    hostinfo)
+        { echo "affinity=$(python -c 'import os;print(len(os.sched_getaffinity(0)))') nproc=$(nproc)";
+          cat /sys/fs/cgroup/cpu.max /sys/fs/cgroup/pids.max 2>&1; lscpu | grep -E "Model name|^CPU\(s\)|NUMA node"; } \
+            > gpurun_out/hostinfo.log 2>&1; cat gpurun_out/hostinfo.log ;;
     hashed)
         run bench_hashed 400 python bench.py --config hashed || exit $?
         run bench_hashed_1M 400 python bench.py --config hashed --chunk 1048576 || exit $? ;;
