@@ -853,11 +853,12 @@ def gather(obj, world):
 def finish(out, rank, world, rec) -> None:
     """Every rank's own record (verified, own time, host submit time) to rank 0,
     which prints the line; exit non-zero on every rank if any rank failed."""
-    from elect_amd import dist
+    from elect_amd import _lib, dist
     recs = gather(rec, world)
     ok = all(r["verified"] for r in recs)
     out["verified"] = ok
     out["ranks"] = recs
+    out["build"] = {"id": _lib.BUILD_ID, "from_these_sources": _lib.BUILD_CURRENT}
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.teardown(world)

@@ -65,6 +65,7 @@ _cp = ctypes.c_void_p
 # (name, restype, argtypes) for every symbol include/elect_ec.h declares.
 SIGNATURES = [
     ("elect_ec_version", ctypes.c_char_p, []),
+    ("elect_ec_build_id", ctypes.c_char_p, []),
     ("elect_ec_strerror", ctypes.c_char_p, [ctypes.c_int]),
     ("elect_ec_device_count", ctypes.c_int, [_ip]),
     ("elect_ec_unaligned_vector_ok", ctypes.c_int, [_ip]),
@@ -120,6 +121,20 @@ for _name, _res, _args in SIGNATURES:
     _f = getattr(lib, _name)
     _f.restype = _res
     _f.argtypes = _args
+
+BUILD_ID = lib.elect_ec_build_id().decode()
+
+
+def _sources_id() -> str | None:
+    try:
+        from .build import build_id
+        return build_id()
+    except OSError:  # sources not shipped beside the library
+        return None
+
+
+# True when the loaded library was built from the sources beside it (by content).
+BUILD_CURRENT = LIB_PATH == os.path.join(HERE, "libelect_ec.so") and BUILD_ID == _sources_id()
 
 
 def strerror(status: int) -> str:

@@ -93,7 +93,12 @@ bool valid_coder(const elect_ec_coder* c) { return c && c->k >= 1 && c->m >= 1; 
 
 extern "C" {
 
-const char* elect_ec_version(void) { return "elect-ec-mi355x 0.1 (gfx950)"; }
+const char* elect_ec_version(void) { return "elect-ec-mi355x 0.2 (gfx950)"; }
+
+#ifndef ELECT_EC_BUILD_ID
+#define ELECT_EC_BUILD_ID "unstamped"
+#endif
+const char* elect_ec_build_id(void) { return ELECT_EC_BUILD_ID; }
 
 const char* elect_ec_strerror(int status)
 {

@@ -71,6 +71,9 @@ typedef struct elect_ec_column {
 } elect_ec_column;
 
 const char* elect_ec_version(void);
+/* Content hash of the sources this library was built from (elect_amd/build.py),
+ * or "unstamped" for builds outside that recipe. */
+const char* elect_ec_build_id(void);
 const char* elect_ec_strerror(int status);
 /* Number of visible HIP devices (0 with ELECT_EC_ENODEV when none). */
 int elect_ec_device_count(int* count);

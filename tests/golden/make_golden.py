@@ -121,6 +121,23 @@ def decode_cases():
         out.append({"k": 4, "m": 2, "L": 0, "decode_indexes": [1, 1, 2, 3], "erased": [0],
                     "mode": "strict" if strict else "compat", "status": rc, "matrix": mat.tobytes().hex(),
                     "outputs": []})
+    # singular survivor sets WITH bytes: libec.so ignores gf_invert_matrix's -1
+    # (EC/erasure_coder.c:257-258) and codes with the partially reduced inverse
+    # (:261-281), so the outputs are defined bytes, not an error; strict refuses.
+    for (k, m), surv, erased in (((4, 2), [1, 1, 2, 3], [0]), ((4, 2), [4, 4, 5, 0], [1]),
+                                 ((4, 2), [0, 1, 2, 2], [3, 4]), ((4, 2), [5, 4, 4, 1], [0, 2]),
+                                 ((8, 4), [2, 2, 3, 4, 5, 6, 7, 8], [0, 1]),
+                                 ((8, 4), [8, 9, 10, 11, 11, 0, 1, 2], [3, 4])):
+        for L in (33, 4099):
+            data = shards("sing", k, L)
+            units = data + o.Encoder(k, m).encode(data)
+            for strict in (False, True):
+                rc, mat = o.decode_matrix(k, m, surv, erased, strict)
+                assert rc == -1
+                outs = [] if strict else o.decode(k, m, [units[i] for i in surv], surv, erased, False)[1]
+                out.append({"k": k, "m": m, "L": L, "decode_indexes": surv, "erased": erased, "input_tag": "sing",
+                            "mode": "strict" if strict else "compat", "status": rc, "singular": True,
+                            "matrix": mat.tobytes().hex(), "outputs": [digest(x) for x in outs]})
     return {"provenance": PROVENANCE, "cases": out}
 
 

@@ -49,6 +49,15 @@ def test_version_and_strerror():
         assert _lib.strerror(st) != "unknown status"
 
 
+def test_library_built_from_these_sources():
+    """The in-tree library's compiled-in build id is the content hash of the
+    sources beside it (elect_amd/build.py): what ships to the GPU box is what
+    the tree says, whatever the file mtimes."""
+    from elect_amd import _lib, build
+    assert _lib.BUILD_ID == build.build_id() == build.stamped_id()
+    assert _lib.BUILD_CURRENT
+
+
 @pytest.mark.parametrize("k,m", [(4, 2), (8, 4), (1, 1), (10, 4), (2, 12), (3, 2)])
 def test_encode_matrix_and_tables_match_oracle(oracle, k, m):
     from elect_amd.coder import RSCoder

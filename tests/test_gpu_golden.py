@@ -46,23 +46,60 @@ def test_golden_encode_on_gpu(dev):
 
 
 def test_golden_decode_on_gpu(dev):
+    """Every decode fixture with bytes, incl. singular survivor sets: compat mode
+    codes them with the partially reduced inverse exactly as libec.so does
+    (EC/erasure_coder.c:257-258 ignores gf_invert_matrix's -1) and reports
+    ELECT_EC_WARN_SINGULAR; strict mode refuses them with ESINGULAR."""
+    from elect_amd import _lib
     from elect_amd.batch import decode_batch, encode_batch
     from elect_amd.coder import RSCoder
     g = load("decode.json")
+    ran_singular = 0
     for c in g["cases"]:
         k, m, L = c["k"], c["m"], c["L"]
         if L == 0:
             continue
         coder = RSCoder(k, m)
-        tag = "elect" if "input_seeds" in c else "dec"
+        tag = c.get("input_tag", "elect" if "input_seeds" in c else "dec")
         st = torch.zeros((1, k + m, L), dtype=torch.uint8, device=dev)
         st[0, :k] = torch.from_numpy(np.stack([_splitmix(seed_of(tag, k, L, j), L) for j in range(k)])).to(dev)
         encode_batch(coder, st[:, :k], st[:, k:])
         out = torch.full((1, len(c["erased"]), L), 0x5A, dtype=torch.uint8, device=dev)
         mode = 1 if c["mode"] == "strict" else 0
+        if c.get("singular") and mode == 1:
+            with pytest.raises(_lib.ECSingularError):
+                decode_batch(coder, st, c["decode_indexes"], c["erased"], out, mode=mode, inputs_by_unit=True)
+            continue
         st_code = decode_batch(coder, st, c["decode_indexes"], c["erased"], out, mode=mode, inputs_by_unit=True)
-        assert st_code == c["status"]
+        assert st_code == (_lib.WARN_SINGULAR if c["status"] == -1 else c["status"])
         assert [digest(x) for x in out.cpu().numpy()[0]] == c["outputs"], c
+        ran_singular += bool(c.get("singular"))
+    assert ran_singular >= 12
+
+
+def test_golden_singular_decode_host_path(dev):
+    """The same singular compat fixtures through the host-memory path (the JNI
+    decodeImpl convention), where libec.so's callers meet them."""
+    from elect_amd import _lib
+    from elect_amd.coder import RSCoder
+    g = load("decode.json")
+    n = 0
+    for c in g["cases"]:
+        if not c.get("singular") or c["mode"] != "compat":
+            continue
+        k, m, L = c["k"], c["m"], c["L"]
+        data = [_splitmix(seed_of("sing", k, L, j), L) for j in range(k)]
+        coder = RSCoder(k, m)
+        par = [np.empty(L, np.uint8) for _ in range(m)]
+        coder.encode_host([d.ctypes.data for d in data], [p.ctypes.data for p in par], L)
+        units = data + par
+        outs = [np.full(L, 0x5A, np.uint8) for _ in c["erased"]]
+        st = coder.decode_host([units[i].ctypes.data for i in c["decode_indexes"]], c["decode_indexes"],
+                               c["erased"], [o.ctypes.data for o in outs], L)
+        assert st == _lib.WARN_SINGULAR
+        assert [digest(x) for x in outs] == c["outputs"], c
+        n += 1
+    assert n >= 12
 
 
 def test_golden_update_on_gpu(dev):

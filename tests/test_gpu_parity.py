@@ -252,23 +252,41 @@ def test_host_path_java_api_roundtrip(dev, oracle):
         dec.release()
 
 
-def test_large_batch_roundtrip_properties(dev):
-    """BASELINE config 2/3 sizes: RS(6,4), 64 KiB, 4096 stripes (1 GiB data).
-    Size-independent checks: decode(encode(x)) == x for every single data
-    erasure, and linearity encode(a ^ b) == encode(a) ^ encode(b)."""
+def _sample(B, extra=6, seed=0):
+    """first, second, middle pair, last two, and a few seeded random stripes"""
+    rng = np.random.default_rng(seed)
+    picks = {0, 1, B // 2 - 1, B // 2, B - 2, B - 1} | {int(x) for x in rng.integers(0, B, extra)}
+    return sorted(p for p in picks if 0 <= p < B)
+
+
+def test_large_batch_roundtrip_properties(dev, oracle):
+    """BASELINE configs[1]/[2] at full size: RS(6,4), 64 KiB, 4096 stripes (1 GiB
+    data) in the bench's [B][k+m][L] layout.  Sampled stripes (first, middle,
+    last: the grid's first and last blocks) byte-for-byte against the oracle for
+    the parity and for every single data erasure's rebuilt unit; every stripe by
+    decode(encode(x)) == x; linearity encode(a ^ b) == encode(a) ^ encode(b)."""
     from elect_amd.batch import decode_batch, encode_batch
     from elect_amd.coder import RSCoder
     k, m, L, B = 4, 2, 65536, 4096
     c = RSCoder(k, m)
+    enc = oracle.Encoder(k, m)
     g = torch.Generator(device=dev).manual_seed(123)
     stripe = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
     stripe[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g)
     encode_batch(c, stripe[:, :k], stripe[:, k:])
+    picks = _sample(B)
+    host = {s: stripe[s].cpu().numpy() for s in picks}
+    for s, h in host.items():
+        want = enc.encode([h[j] for j in range(k)])
+        assert all(np.array_equal(h[k + r], want[r]) for r in range(m)), s
     out = torch.empty((B, 1, L), dtype=torch.uint8, device=dev)
     for e in range(k):
         surv = [i for i in range(k + m) if i != e][:k]
         decode_batch(c, stripe, surv, [e], out, inputs_by_unit=True)
         assert torch.equal(out[:, 0], stripe[:, e])
+        for s in picks:
+            rc, want = oracle.decode(k, m, [host[s][i] for i in surv], surv, [e])
+            assert rc == 0 and np.array_equal(out[s, 0].cpu().numpy(), want[0]), (e, s)
     del out
     a = stripe[: B // 4, :k].clone()
     b = torch.randint(0, 256, a.shape, dtype=torch.uint8, device=dev, generator=g)
