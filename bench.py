@@ -87,6 +87,11 @@ def parse():
     ap.add_argument("--host-op", choices=("encode", "encode_ex"), default="encode",
                     help="hostpath: plain encode (the JNI encodeImpl), or ELECT's fused encode step "
                          "(encodeExImpl: content = codeLength/1.05, parity hashCodes)")
+    ap.add_argument("--flows-tile", type=int, default=-1,
+                    help="flows: tile bytes for the [B][T][k+m][tile] layout (-1: 64 KiB tiles above 64 KiB, "
+                         "0: untiled)")
+    ap.add_argument("--flows-inplace", action="store_true",
+                    help="flows: the update writes the new parity over the old (ELECT writes separate buffers)")
     ap.add_argument("--graph", action="store_true",
                     help="headline and mixed: capture each step's launches in a HIP graph and replay it")
     ap.add_argument("--launch-check", action="store_true",
@@ -754,86 +759,150 @@ def config_flows(args, world, rank, dev):
     encode, parity hashCode), parity update (ECParityUpdateVerbHandler.java:
     634-699: old/new zero filled, encodeUpdate in place, new-parity hashCode) and
     degraded read (ECRecovery.java:128-141: survivors zero filled, decode of the
-    updated unit).  RS(6,4), codeLength --chunk, --stripes per GPU in one
-    [B][k+m][L] block; contents fill 1/1.05 of codeLength less up to 5 %
-    (codeLength = ceil(1.05 x SSTable size), StorageService.java:331-339)."""
-    from elect_amd.batch import decode_batch_ex, encode_batch, encode_batch_ex, encode_update_batch_ex
+    unit the update replaces).  The update writes its new parity to separate
+    buffers as ELECT does (newParityCodes, ECParityUpdateVerbHandler.java:664-688;
+    --flows-inplace: over the old parity instead).  RS(6,4), codeLength --chunk,
+    --stripes per GPU in one block;
+    contents fill 1/1.05 of codeLength less up to 5 % (codeLength = ceil(1.05 x
+    SSTable size), StorageService.java:331-339).  Layout: codeLengths above 64 KiB
+    are stored as 64 KiB tiles [B][T][k+m][64K] (T = ceil(L / 64K); --flows-tile 0:
+    untiled [B][k+m][pitch], the pitch rounded up to 256 B) and coded through the
+    elect_ec_*_batch_tiled calls: every unit is then 64 KiB back to back, the
+    layout HBM streams best, whatever ELECT's codeLength is."""
+    from elect_amd.batch import (decode_batch_ex, decode_batch_tiled, encode_batch, encode_batch_ex,
+                                 encode_batch_tiled, encode_update_batch_ex, encode_update_batch_tiled)
     from elect_amd.coder import RSCoder, java_bytebuffer_hash
     k, m, L, B = 4, 2, args.chunk, args.stripes
+    n = k + m
     coder = RSCoder(k, m)
     g = torch.Generator(device=dev)
     g.manual_seed(0xE1EC7)
-    # units at a 256-byte pitch (DESIGN.md §3: a codeLength like 4,404,020 B, = 4 mod 16, would
-    # otherwise put every unit start off 16-byte alignment)
-    pitch = (L + 255) & ~255
-    stripe = torch.empty((B, k + m, pitch), dtype=torch.uint8, device=dev)[:, :, :L]
-    data, par = stripe[:, :k], stripe[:, k:]
-    data.copy_(torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g))
+    tile = args.flows_tile if args.flows_tile >= 0 else (TILE if L > TILE else 0)
+    if tile:
+        T = -(-L // tile)
+        blk = torch.empty((B, T, n, tile), dtype=torch.uint8, device=dev)
+        view = blk.view(B * T, n, tile)
+
+        def scatter(dst_view, src_logical):  # [B, c, L] -> tiles of dst_view ([B*T, c, tile])
+            c = src_logical.shape[1]
+            full = torch.zeros((B, c, T * tile), dtype=torch.uint8, device=dev)
+            full[:, :, :L] = src_logical
+            dst_view.copy_(full.view(B, c, T, tile).permute(0, 2, 1, 3).reshape(B * T, c, tile))
+
+        def gather(src_view):  # tiles -> [B, c, L]
+            c = src_view.shape[1]
+            return src_view.reshape(B, T, c, tile).permute(0, 2, 1, 3).reshape(B, c, T * tile)[:, :, :L]
+        layout = f"[B][{T}][k+m][{tile}] (64 KiB tiles, {T * tile - L} B pad per unit)"
+    else:
+        pitch = (L + 255) & ~255  # 256-byte unit pitch: ELECT's 4,404,020 B (= 4 mod 16) would misalign units
+        stripe = torch.empty((B, n, pitch), dtype=torch.uint8, device=dev)[:, :, :L]
+        layout = f"[B][k+m][{pitch}] (unit pitch rounded up to 256 B)"
     top = int(L / 1.05)
+    src = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=g)
     lens = torch.randint(int(top * 0.95), top + 1, (B, k), dtype=torch.int32, device=dev, generator=g)
-    new = torch.empty((B, pitch), dtype=torch.uint8, device=dev)[:, :L]
-    new.copy_(torch.randint(0, 256, (B, L), dtype=torch.uint8, device=dev, generator=g))
+    new_l = torch.randint(0, 256, (B, L), dtype=torch.uint8, device=dev, generator=g)
     t = 1
     ulens = torch.stack([lens[:, t], torch.randint(int(top * 0.95), top + 1, (B,), dtype=torch.int32, device=dev,
                                                    generator=g)], dim=1).contiguous()
     surv = [j for j in range(k) if j != t] + [k]  # degraded read of unit t from the others + parity 0
     dlens = torch.cat([lens[:, [j for j in range(k) if j != t]],
                        torch.full((B, 1), L, dtype=torch.int32, device=dev)], dim=1).contiguous()
-    rebuilt = torch.empty((B, 1, pitch), dtype=torch.uint8, device=dev)[:, :, :L]
     h_enc = torch.empty((B, m), dtype=torch.int32, device=dev)
     h_upd = torch.empty((B, m), dtype=torch.int32, device=dev)
+    if tile:
+        scatter(view[:, :k], src)
+        new = torch.empty((B * T, 1, tile), dtype=torch.uint8, device=dev)
+        scatter(new, new_l[:, None])
+        new = new[:, 0]
+        rebuilt = torch.empty((B * T, 1, tile), dtype=torch.uint8, device=dev)
+        data, par = view[:, :k], view[:, k:]
+        par_new = par if args.flows_inplace else torch.empty((B * T, m, tile), dtype=torch.uint8, device=dev)
+
+        def enc_step():
+            encode_batch_tiled(coder, data, par, L, lengths=lens, hashes=h_enc)
+
+        def upd_step():
+            encode_update_batch_tiled(coder, t, view[:, t], new, par, par_new, L, lengths=ulens, hashes=h_upd)
+
+        def dec_step():
+            decode_batch_tiled(coder, view, surv, [t], rebuilt, L, lengths=dlens, inputs_by_unit=True)
+    else:
+        stripe[:, :k] = src
+        data, par = stripe[:, :k], stripe[:, k:]
+        new = torch.empty((B, (L + 255) & ~255), dtype=torch.uint8, device=dev)[:, :L]
+        new.copy_(new_l)
+        rebuilt = torch.empty((B, 1, (L + 255) & ~255), dtype=torch.uint8, device=dev)[:, :, :L]
+        par_new = par if args.flows_inplace else \
+            torch.empty((B, m, (L + 255) & ~255), dtype=torch.uint8, device=dev)[:, :, :L]
+
+        def enc_step():
+            encode_batch_ex(coder, data, par, lengths=lens, hashes=h_enc)
+
+        def upd_step():
+            encode_update_batch_ex(coder, t, data[:, t], new, par, par_new, lengths=ulens, hashes=h_upd)
+
+        def dec_step():
+            decode_batch_ex(coder, stripe, surv, [t], rebuilt, lengths=dlens, inputs_by_unit=True)
     ev = {"encode": [], "update": [], "decode": []}
 
     def step():
         es = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         es[0].record()
-        encode_batch_ex(coder, data, par, lengths=lens, hashes=h_enc)
+        enc_step()
         es[1].record()
-        encode_update_batch_ex(coder, t, data[:, t], new, par, par, lengths=ulens, hashes=h_upd)
+        upd_step()
         es[2].record()
-        decode_batch_ex(coder, stripe, surv, [t], rebuilt, lengths=dlens, inputs_by_unit=True)
+        dec_step()
         es[3].record()
-        for i, n in enumerate(("encode", "update", "decode")):
-            ev[n].append((es[i], es[i + 1]))
+        for i, nm in enumerate(("encode", "update", "decode")):
+            ev[nm].append((es[i], es[i + 1]))
 
     dt, submit = timed(step, args.steps, args.warmup, world)
-    ms = {n: sum(a.elapsed_time(b) for a, b in v[-args.steps:]) / args.steps for n, v in ev.items()}
-    # self-check through the product: the updated parity is the encode of the new zero-filled
-    # stripe, its hashes match, and the degraded read returns the new unit zero filled
+    ms = {nm: sum(a.elapsed_time(b) for a, b in v[-args.steps:]) / args.steps for nm, v in ev.items()}
+    # self-check through the product (coded untiled, contiguous): the new parity is the
+    # encode of the zero-filled stripe with unit t replaced, its hashes match, and the
+    # degraded read returns the unit t its parity holds, zero filled
     idx = torch.arange(L, device=dev).view(1, L)
     zero = torch.zeros((), dtype=torch.uint8, device=dev)
-    filled = torch.where(idx.view(1, 1, L) < lens.view(B, k, 1), data, zero)
-    filled[:, t] = torch.where(idx < ulens[:, 1:2], new, zero)
-    ref = torch.empty_like(par)
+    filled = torch.where(idx.view(1, 1, L) < lens.view(B, k, 1), src, zero)
+    old_t = filled[:, t].clone()
+    filled[:, t] = torch.where(idx < ulens[:, 1:2], new_l, zero)
+    ref = torch.empty((B, m, L), dtype=torch.uint8, device=dev)
     encode_batch(coder, filled, ref)
+    par_l = gather(par_new) if tile else par_new
+    reb_l = gather(rebuilt)[:, 0] if tile else rebuilt[:, 0]
     h = h_upd.cpu()
-    ok = torch.equal(par, ref) and all(int(h[s, r]) == java_bytebuffer_hash(ref[s, r].cpu().numpy())
-                                       for s, r in ((0, 0), (B - 1, m - 1)))
-    ok = ok and torch.equal(rebuilt[:, 0], filled[:, t])
+    ok = torch.equal(par_l, ref) and all(int(h[s, r]) == java_bytebuffer_hash(ref[s, r].cpu().numpy())
+                                         for s, r in ((0, 0), (B - 1, m - 1)))
+    ok = ok and torch.equal(reb_l, filled[:, t] if args.flows_inplace else old_t)
+    if tile:  # the output pad of every unit's last tile is written as zero
+        ok = ok and not bool(par_new.reshape(B, T, m, tile)[:, -1, :, L - (T - 1) * tile:].any())
     valid = int(lens.sum().item())
     uvalid = int(ulens.sum().item())
     dvalid = int(dlens.sum().item())
     alg = {"encode": valid + B * m * L, "update": uvalid + 2 * B * m * L, "decode": dvalid + B * L}
     kern = {}
-    for n in ("encode", "update", "decode"):
-        gbs = alg[n] / (ms[n] * 1e-3) / 1e9
-        kern[n] = {"ms": round(ms[n], 4), "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-                   "algorithmic_bytes_per_launch": alg[n]}
+    for nm in ("encode", "update", "decode"):
+        gbs = alg[nm] / (ms[nm] * 1e-3) / 1e9
+        kern[nm] = {"ms": round(ms[nm], 4), "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                    "algorithmic_bytes_per_launch": alg[nm]}
     return {"metric": "GiB/s device-resident ELECT coding steps (padded+hashed encode, padded+hashed update, "
                       "padded degraded-read decode), RS(6,4)",
             "value": round(world * args.steps * B * (2 * k + 1) * L / dt / GIB, 2),
             "unit": "GiB/s (codeLength bytes: k units encoded + 1 updated + k survivors decoded per stripe)",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(dt / args.steps * 1e3, 4), "host_submit_ms_per_step": round(submit, 4),
+            "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok, "kernels": kern,
             "roofline": {"bound": "hbm", "achieved": kern["encode"]["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": kern["encode"]["frac"], "traffic": None,
                          "kernel": "gf_apply_x16<4,2,PAD,HASH> (encode step)",
                          "algorithmic_bytes_per_launch": alg["encode"],
                          "fill": round(valid / (B * k * L), 3)},
-            "config": {"workload": f"{B} stripes x {L} B codeLength per GPU; encode all, update unit {t} in place, "
-                                   f"rebuild unit {t} from units {surv}", "layout": f"[B][k+m][{pitch}] (unit pitch "
-                                   "rounded up to 256 B)", "parallelism": f"stripe-partitioned x{world}"}}
+            "config": {"workload": f"{B} stripes x {L} B codeLength per GPU; encode all, update unit {t} "
+                                   f"({'in place' if args.flows_inplace else 'new parity to separate buffers'}), "
+                                   f"rebuild unit {t} from units {surv}", "layout": layout,
+                       "parallelism": f"stripe-partitioned x{world}"}}
 
 
 def launch_check(args, world, rank):

@@ -107,6 +107,14 @@ SIGNATURES = [
                                                        ColumnT, ColumnT, _cp, Shards, Shards, _cp, _cp]),
     ("elect_ec_decode_batch_ex", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, Shards, _cp, _ip, _ip,
                                                 ctypes.c_int, Shards, ctypes.c_uint, ctypes.c_int, _cp]),
+    ("elect_ec_encode_batch_tiled", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, Shards,
+                                                   _cp, Shards, _cp, _cp]),
+    ("elect_ec_encode_update_batch_tiled", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                                          ctypes.c_int, ColumnT, ColumnT, _cp, Shards, Shards, _cp,
+                                                          _cp]),
+    ("elect_ec_decode_batch_tiled", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, Shards,
+                                                   _cp, _ip, _ip, ctypes.c_int, Shards, ctypes.c_uint, ctypes.c_int,
+                                                   _cp]),
     ("elect_ec_apply_batch", ctypes.c_int, [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
                                             ctypes.c_size_t, ctypes.POINTER(ColumnT),
                                             ctypes.POINTER(ColumnT), _cp]),

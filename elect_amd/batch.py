@@ -153,6 +153,58 @@ def encode_update_batch_ex(coder: RSCoder, target: int, old: torch.Tensor, new: 
           "encode_update_batch_ex")
 
 
+def _tiles_of(chunk_size: int, tile: int, rows: int) -> int:
+    """Stripes in a tiled batch whose coding view has `rows` tile rows."""
+    t = max(1, -(-chunk_size // tile))
+    if tile <= 0 or rows % t:
+        raise ValueError(f"a tiled view needs a multiple of {t} tile rows (ceil({chunk_size}/{tile})), got {rows}")
+    return rows // t
+
+
+def encode_batch_tiled(coder: RSCoder, data: torch.Tensor, parity: torch.Tensor, chunk_size: int, lengths=None,
+                       hashes=None, stream=None) -> None:
+    """encode_batch_ex over tiled units: data [B*T, k, tile] / parity [B*T, m, tile] views
+    where stripe s's unit j is tiles s*T .. s*T+T-1 of column j (T = ceil(chunk_size/tile));
+    lengths [B, k] and hashes [B, m] are per stripe (include/elect_ec.h, tiled units)."""
+    rows, k, tile = data.shape
+    B = _tiles_of(chunk_size, tile, rows)
+    if k != coder.k or parity.shape != (rows, coder.m, tile):
+        raise ValueError(f"shape mismatch: data {tuple(data.shape)} parity {tuple(parity.shape)}")
+    check(lib.elect_ec_encode_batch_tiled(coder.handle, chunk_size, tile, B, _shards(data),
+                                          _lengths(lengths, B, k, data.device), _shards(parity),
+                                          _hashes(hashes, B, coder.m, data.device), _stream(stream)),
+          "encode_batch_tiled")
+
+
+def encode_update_batch_tiled(coder: RSCoder, target: int, old: torch.Tensor, new: torch.Tensor,
+                              parity_in: torch.Tensor, parity_out: torch.Tensor, chunk_size: int, lengths=None,
+                              hashes=None, stream=None) -> None:
+    """encode_update_batch_ex over tiled units: old/new [B*T, tile], parity [B*T, m, tile]."""
+    rows, tile = old.shape
+    B = _tiles_of(chunk_size, tile, rows)
+    check(lib.elect_ec_encode_update_batch_tiled(coder.handle, chunk_size, tile, B, target, _column(old), _column(new),
+                                                 _lengths(lengths, B, 2, old.device), _shards(parity_in),
+                                                 _shards(parity_out), _hashes(hashes, B, coder.m, old.device),
+                                                 _stream(stream)),
+          "encode_update_batch_tiled")
+
+
+def decode_batch_tiled(coder: RSCoder, inputs: torch.Tensor, decode_indexes, erased, outputs: torch.Tensor,
+                       chunk_size: int, lengths=None, mode: int = _lib.DECODE_COMPAT, inputs_by_unit: bool = False,
+                       outputs_by_unit: bool = False, stream=None) -> int:
+    """decode_batch_ex over tiled units: inputs [B*T, k or k+m, tile], outputs [B*T, e or k+m, tile]."""
+    rows, _, tile = inputs.shape
+    B = _tiles_of(chunk_size, tile, rows)
+    flags = (_lib.INPUTS_BY_UNIT if inputs_by_unit else 0) | (_lib.OUTPUTS_BY_UNIT if outputs_by_unit else 0)
+    if len(decode_indexes) != coder.k:
+        raise ValueError("decode_indexes needs exactly k entries")
+    return check(lib.elect_ec_decode_batch_tiled(coder.handle, chunk_size, tile, B, _shards(inputs),
+                                                 _lengths(lengths, B, coder.k, inputs.device),
+                                                 int_array(decode_indexes), int_array(erased), len(erased),
+                                                 _shards(outputs), flags, mode, _stream(stream)),
+                 "decode_batch_tiled")
+
+
 def apply_batch(coef: np.ndarray, src, dst, stream=None) -> None:
     """dst[r] = XOR_j coef[r, j] * src[j] over [B, L] column tensors."""
     coef = np.ascontiguousarray(coef, np.uint8)

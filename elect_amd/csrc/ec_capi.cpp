@@ -89,6 +89,133 @@ hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
 
 bool valid_coder(const elect_ec_coder* c) { return c && c->k >= 1 && c->m >= 1; }
 
+// Batch geometry: num_stripes units of chunk_size bytes, untiled (tile == 0) or
+// stored as ceil(chunk_size / tile) tiles of `tile` bytes, each tile coded as a
+// stripe of its own (kern::ApplyParams::tiles).  Tiled launches always run the
+// padded kernels: columns without explicit lengths hold chunk_size bytes.
+int set_geometry(ApplyParams& p, size_t chunk_size, size_t tile, size_t num_stripes)
+{
+    p.len = chunk_size;
+    p.stripes = num_stripes;
+    if (tile == 0) return ELECT_EC_OK;
+    if (tile % 16 || tile > 0x7FFFFFFFull || chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
+    const uint64_t t = std::max<uint64_t>(1, (chunk_size + tile - 1) / tile);
+    if (t > 0xFFFFFFFFull || num_stripes > ~uint64_t{0} / t) return ELECT_EC_EINVAL;
+    p.len = tile;
+    p.stripes = num_stripes * t;
+    p.tiles = static_cast<uint32_t>(t);
+    p.unit_len = chunk_size;
+    p.padded = true;
+    for (int j = 0; j < elect::kern::kMaxCols; ++j) p.clen[j] = static_cast<uint32_t>(chunk_size);
+    return ELECT_EC_OK;
+}
+
+int encode_batch_impl(const elect_ec_coder* coder, size_t chunk_size, size_t tile, size_t num_stripes,
+                      elect_ec_shards data, const uint32_t* d_data_lengths, elect_ec_shards parity,
+                      int32_t* d_hashes, void* stream)
+{
+    if (!valid_coder(coder)) return ELECT_EC_EINVAL;
+    if ((d_data_lengths || tile) && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
+    if (num_stripes == 0 || (chunk_size == 0 && !d_hashes)) return ELECT_EC_OK;
+    if (chunk_size > 0 && (!data.base || !parity.base)) return ELECT_EC_EINVAL;
+    ApplyParams p;
+    const int g = set_geometry(p, chunk_size, tile, num_stripes);
+    if (g != ELECT_EC_OK) return g;
+    p.cols = coder->k;
+    p.rows = coder->m;
+    if (d_data_lengths) {
+        p.padded = true;
+        p.lens = d_data_lengths;
+    }
+    if (d_hashes) {
+        p.hash_seed = true;  // the launcher produces 31^len + sum (no separate memset where it can)
+        p.hashes = d_hashes;
+        p.hash_stride = static_cast<uint32_t>(coder->m);
+    }
+    for (int j = 0; j < p.cols; ++j) p.src[j] = col(data.base, data.stripe_stride, j * data.shard_stride);
+    for (int r = 0; r < p.rows; ++r) {
+        p.dst[r] = col(parity.base, parity.stripe_stride, r * parity.shard_stride);
+        std::memcpy(p.coef + r * p.cols, parity_row(coder, r), coder->k);
+    }
+    return map_hip(elect::kern::launch_apply(p, as_stream(stream)));
+}
+
+int decode_batch_impl(const elect_ec_coder* coder, size_t chunk_size, size_t tile, size_t num_stripes,
+                      elect_ec_shards inputs, const uint32_t* d_input_lengths, const int* decode_indexes,
+                      const int* erased_indexes, int num_erased, elect_ec_shards outputs, unsigned flags, int mode,
+                      void* stream)
+{
+    if (!valid_coder(coder)) return ELECT_EC_EINVAL;
+    if ((d_input_lengths || tile) && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
+    ApplyParams p;
+    const int st = build_decode_matrix(coder, decode_indexes, erased_indexes, num_erased, mode, p.coef);
+    if (st < 0) return st;
+    if (num_erased == 0 || chunk_size == 0 || num_stripes == 0) return st;
+    if (!inputs.base || !outputs.base) return ELECT_EC_EINVAL;
+    const int g = set_geometry(p, chunk_size, tile, num_stripes);
+    if (g != ELECT_EC_OK) return g;
+    p.cols = coder->k;
+    p.rows = num_erased;
+    for (int j = 0; j < p.cols; ++j) {
+        const size_t slot = (flags & ELECT_EC_INPUTS_BY_UNIT) ? static_cast<size_t>(decode_indexes[j]) : j;
+        p.src[j] = col(inputs.base, inputs.stripe_stride, slot * inputs.shard_stride);
+    }
+    for (int r = 0; r < p.rows; ++r) {
+        const size_t slot = (flags & ELECT_EC_OUTPUTS_BY_UNIT) ? static_cast<size_t>(erased_indexes[r]) : r;
+        p.dst[r] = col(outputs.base, outputs.stripe_stride, slot * outputs.shard_stride);
+    }
+    if (d_input_lengths) {
+        p.padded = true;
+        p.lens = d_input_lengths;
+    }
+    const int rc = map_hip(elect::kern::launch_apply(p, as_stream(stream)));
+    return rc != ELECT_EC_OK ? rc : st;
+}
+
+// The update as a (2+m)-column product [c_r, c_r, e_r] over [old, new, P...]
+// (see elect_ec_encode_update_ex): the padded, hashed and tiled encode machinery
+// serves it unchanged.
+int update_batch_impl(const elect_ec_coder* coder, size_t chunk_size, size_t tile, size_t num_stripes,
+                      int target_data_index, elect_ec_column old_data, elect_ec_column new_data,
+                      const uint32_t* d_old_new_lengths, elect_ec_shards parity_in, elect_ec_shards parity_out,
+                      int32_t* d_hashes, void* stream)
+{
+    if (!valid_coder(coder) || target_data_index < 0 || target_data_index >= coder->k) return ELECT_EC_EINVAL;
+    if (d_hashes && 2 + coder->m > ELECT_EC_MAX_DATA_UNITS) return ELECT_EC_EINVAL;
+    if ((d_old_new_lengths || tile) && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
+    if (num_stripes == 0 || (chunk_size == 0 && !d_hashes)) return ELECT_EC_OK;
+    if (chunk_size > 0 && (!old_data.ptr || !new_data.ptr || !parity_in.base || !parity_out.base))
+        return ELECT_EC_EINVAL;
+    ApplyParams p;
+    const int g = set_geometry(p, chunk_size, tile, num_stripes);
+    if (g != ELECT_EC_OK) return g;
+    p.cols = 2 + coder->m;
+    p.rows = coder->m;
+    p.src[0] = col(old_data.ptr, old_data.stripe_stride, 0);
+    p.src[1] = col(new_data.ptr, new_data.stripe_stride, 0);
+    for (int r = 0; r < p.rows; ++r) {
+        p.src[2 + r] = col(parity_in.base, parity_in.stripe_stride, r * parity_in.shard_stride);
+        p.dst[r] = col(parity_out.base, parity_out.stripe_stride, r * parity_out.shard_stride);
+        const uint8_t c = parity_row(coder, r)[target_data_index];
+        p.coef[r * p.cols + 0] = c;
+        p.coef[r * p.cols + 1] = c;
+        p.coef[r * p.cols + 2 + r] = 1;
+    }
+    if (d_old_new_lengths) {  // old/new padded; the old parity is full length
+        p.padded = true;
+        p.lens = d_old_new_lengths;
+        p.lens_cols = 2;
+        p.lens_stride = 2;
+        for (int r = 0; r < p.rows; ++r) p.clen[2 + r] = static_cast<uint32_t>(chunk_size);
+    }
+    if (d_hashes) {
+        p.hash_seed = true;
+        p.hashes = d_hashes;
+        p.hash_stride = static_cast<uint32_t>(coder->m);
+    }
+    return map_hip(elect::kern::launch_apply(p, as_stream(stream)));
+}
+
 }  // namespace
 
 extern "C" {
@@ -336,30 +463,16 @@ int elect_ec_encode_batch_ex(const elect_ec_coder* coder, size_t chunk_size, siz
                              elect_ec_shards data, const uint32_t* d_data_lengths, elect_ec_shards parity,
                              int32_t* d_hashes, void* stream)
 {
-    if (!valid_coder(coder)) return ELECT_EC_EINVAL;
-    if (d_data_lengths && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
-    if (num_stripes == 0 || (chunk_size == 0 && !d_hashes)) return ELECT_EC_OK;
-    if (chunk_size > 0 && (!data.base || !parity.base)) return ELECT_EC_EINVAL;
-    ApplyParams p;
-    p.len = chunk_size;
-    p.stripes = num_stripes;
-    p.cols = coder->k;
-    p.rows = coder->m;
-    if (d_data_lengths) {
-        p.padded = true;
-        p.lens = d_data_lengths;
-    }
-    if (d_hashes) {
-        p.hash_seed = true;  // the launcher produces 31^len + sum (no separate memset where it can)
-        p.hashes = d_hashes;
-        p.hash_stride = static_cast<uint32_t>(coder->m);
-    }
-    for (int j = 0; j < p.cols; ++j) p.src[j] = col(data.base, data.stripe_stride, j * data.shard_stride);
-    for (int r = 0; r < p.rows; ++r) {
-        p.dst[r] = col(parity.base, parity.stripe_stride, r * parity.shard_stride);
-        std::memcpy(p.coef + r * p.cols, parity_row(coder, r), coder->k);
-    }
-    return map_hip(elect::kern::launch_apply(p, as_stream(stream)));
+    return encode_batch_impl(coder, chunk_size, 0, num_stripes, data, d_data_lengths, parity, d_hashes, stream);
+}
+
+int elect_ec_encode_batch_tiled(const elect_ec_coder* coder, size_t chunk_size, size_t tile_bytes,
+                                size_t num_stripes, elect_ec_shards data, const uint32_t* d_data_lengths,
+                                elect_ec_shards parity, int32_t* d_hashes, void* stream)
+{
+    if (tile_bytes == 0) return ELECT_EC_EINVAL;
+    return encode_batch_impl(coder, chunk_size, tile_bytes, num_stripes, data, d_data_lengths, parity, d_hashes,
+                             stream);
 }
 
 int elect_ec_encode_batch_padded(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
@@ -390,31 +503,18 @@ int elect_ec_decode_batch_ex(const elect_ec_coder* coder, size_t chunk_size, siz
                              const int* erased_indexes, int num_erased, elect_ec_shards outputs, unsigned flags,
                              int mode, void* stream)
 {
-    if (!valid_coder(coder)) return ELECT_EC_EINVAL;
-    if (d_input_lengths && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
-    ApplyParams p;
-    const int st = build_decode_matrix(coder, decode_indexes, erased_indexes, num_erased, mode, p.coef);
-    if (st < 0) return st;
-    if (num_erased == 0 || chunk_size == 0 || num_stripes == 0) return st;
-    if (!inputs.base || !outputs.base) return ELECT_EC_EINVAL;
-    p.len = chunk_size;
-    p.stripes = num_stripes;
-    p.cols = coder->k;
-    p.rows = num_erased;
-    for (int j = 0; j < p.cols; ++j) {
-        const size_t slot = (flags & ELECT_EC_INPUTS_BY_UNIT) ? static_cast<size_t>(decode_indexes[j]) : j;
-        p.src[j] = col(inputs.base, inputs.stripe_stride, slot * inputs.shard_stride);
-    }
-    for (int r = 0; r < p.rows; ++r) {
-        const size_t slot = (flags & ELECT_EC_OUTPUTS_BY_UNIT) ? static_cast<size_t>(erased_indexes[r]) : r;
-        p.dst[r] = col(outputs.base, outputs.stripe_stride, slot * outputs.shard_stride);
-    }
-    if (d_input_lengths) {
-        p.padded = true;
-        p.lens = d_input_lengths;
-    }
-    const int rc = map_hip(elect::kern::launch_apply(p, as_stream(stream)));
-    return rc != ELECT_EC_OK ? rc : st;
+    return decode_batch_impl(coder, chunk_size, 0, num_stripes, inputs, d_input_lengths, decode_indexes,
+                             erased_indexes, num_erased, outputs, flags, mode, stream);
+}
+
+int elect_ec_decode_batch_tiled(const elect_ec_coder* coder, size_t chunk_size, size_t tile_bytes,
+                                size_t num_stripes, elect_ec_shards inputs, const uint32_t* d_input_lengths,
+                                const int* decode_indexes, const int* erased_indexes, int num_erased,
+                                elect_ec_shards outputs, unsigned flags, int mode, void* stream)
+{
+    if (tile_bytes == 0) return ELECT_EC_EINVAL;
+    return decode_batch_impl(coder, chunk_size, tile_bytes, num_stripes, inputs, d_input_lengths, decode_indexes,
+                             erased_indexes, num_erased, outputs, flags, mode, stream);
 }
 
 int elect_ec_encode_update_batch(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
@@ -447,40 +547,19 @@ int elect_ec_encode_update_batch_ex(const elect_ec_coder* coder, size_t chunk_si
     if (!d_old_new_lengths && !d_hashes)
         return elect_ec_encode_update_batch(coder, chunk_size, num_stripes, target_data_index, old_data, new_data,
                                             parity_in, parity_out, stream);
-    if (d_hashes && 2 + coder->m > ELECT_EC_MAX_DATA_UNITS) return ELECT_EC_EINVAL;
-    if (d_old_new_lengths && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
-    if (num_stripes == 0 || (chunk_size == 0 && !d_hashes)) return ELECT_EC_OK;
-    if (chunk_size > 0 && (!old_data.ptr || !new_data.ptr || !parity_in.base || !parity_out.base))
-        return ELECT_EC_EINVAL;
-    // [c_r, c_r, e_r] over [old, new, P...] (see elect_ec_encode_update_ex).
-    ApplyParams p;
-    p.len = chunk_size;
-    p.stripes = num_stripes;
-    p.cols = 2 + coder->m;
-    p.rows = coder->m;
-    p.src[0] = col(old_data.ptr, old_data.stripe_stride, 0);
-    p.src[1] = col(new_data.ptr, new_data.stripe_stride, 0);
-    for (int r = 0; r < p.rows; ++r) {
-        p.src[2 + r] = col(parity_in.base, parity_in.stripe_stride, r * parity_in.shard_stride);
-        p.dst[r] = col(parity_out.base, parity_out.stripe_stride, r * parity_out.shard_stride);
-        const uint8_t c = parity_row(coder, r)[target_data_index];
-        p.coef[r * p.cols + 0] = c;
-        p.coef[r * p.cols + 1] = c;
-        p.coef[r * p.cols + 2 + r] = 1;
-    }
-    if (d_old_new_lengths) {  // old/new padded; the old parity is full length
-        p.padded = true;
-        p.lens = d_old_new_lengths;
-        p.lens_cols = 2;
-        p.lens_stride = 2;
-        for (int r = 0; r < p.rows; ++r) p.clen[2 + r] = static_cast<uint32_t>(chunk_size);
-    }
-    if (d_hashes) {
-        p.hash_seed = true;
-        p.hashes = d_hashes;
-        p.hash_stride = static_cast<uint32_t>(coder->m);
-    }
-    return map_hip(elect::kern::launch_apply(p, as_stream(stream)));
+    return update_batch_impl(coder, chunk_size, 0, num_stripes, target_data_index, old_data, new_data,
+                             d_old_new_lengths, parity_in, parity_out, d_hashes, stream);
+}
+
+int elect_ec_encode_update_batch_tiled(const elect_ec_coder* coder, size_t chunk_size, size_t tile_bytes,
+                                       size_t num_stripes, int target_data_index, elect_ec_column old_data,
+                                       elect_ec_column new_data, const uint32_t* d_old_new_lengths,
+                                       elect_ec_shards parity_in, elect_ec_shards parity_out, int32_t* d_hashes,
+                                       void* stream)
+{
+    if (tile_bytes == 0) return ELECT_EC_EINVAL;
+    return update_batch_impl(coder, chunk_size, tile_bytes, num_stripes, target_data_index, old_data, new_data,
+                             d_old_new_lengths, parity_in, parity_out, d_hashes, stream);
 }
 
 int elect_ec_apply_batch(const unsigned char* coef, int rows, int cols, size_t chunk_size, size_t num_stripes,

@@ -270,6 +270,14 @@ int host_device(int ndev, int* dev)
 // ([slot][cols][pitch] layout) and ONE D2H, then each caller copies its outputs
 // (and parity hashes) out.  Encodes, decodes and parity updates (as products)
 // all batch.  Two arenas alternate, so one fills while the other is in flight.
+//
+// Units longer than 64 KiB are stored in the arena as 64 KiB tiles,
+// [slot][T][cols][64 KiB] with T = ceil(len / 64 KiB), and coded through the
+// tiled launch (kern::ApplyParams::tiles): every unit is then 64 KiB back to
+// back, the layout HBM streams best, whatever ELECT's codeLength
+// (4,404,020 B -> 68 tiles).  Callers copy their units tile by tile; the pad
+// past len in each unit's last tile is never read (the tiled launch always
+// runs the padded kernels, content = len or the caller's lengths).
 // ---------------------------------------------------------------------------
 struct BatchConfig {
     std::atomic<int> enabled{-1};  // -1: read ELECT_EC_BATCH on first use
@@ -294,8 +302,9 @@ BatchConfig& batch_config()
 
 class Batcher {
 public:
-    static constexpr int kFallback = 1000;  // request does not fit: run it directly
+    static constexpr int kFallback = 1000;  // request does not fit (or no arena): run it directly
     static constexpr int kSlabs = 2;
+    static constexpr size_t kTile = size_t{1} << 16;
     // Per-slot content lengths (padded ops) and parity hashes (hashed ops) of a
     // batch: entries per arena, which caps such a batch's stripes.
     static constexpr size_t kMetaEntries = size_t{1} << 16;
@@ -304,15 +313,21 @@ public:
 
     int submit(const HostOp& op, size_t len)
     {
-        const size_t pitch = (len + 255) & ~size_t{255};
+        // untiled: one unit per column at a 256-byte pitch; tiled: T tiles of 64 KiB
+        const size_t tiles = len > kTile ? (len + kTile - 1) / kTile : 1;
+        const size_t pitch = tiles > 1 ? kTile : (len + 255) & ~size_t{255};
         std::unique_lock<std::mutex> lock(mu_);
+        if (init_failed_) return kFallback;
         if (!started_) {  // arenas, streams and events once, before anything is in flight
-            const int rc = init(batch_config().arena_bytes.load());
-            if (rc != ELECT_EC_OK) return rc;
+            if (init(batch_config().arena_bytes.load()) != ELECT_EC_OK) {
+                release();  // whatever the failed attempt got; callers use the per-thread engine
+                init_failed_ = true;
+                return kFallback;
+            }
             std::thread(&Batcher::worker, this).detach();  // lives as long as the process
             started_ = true;
         }
-        if (static_cast<size_t>(op.cols) * pitch > arena_ || static_cast<size_t>(op.rows) * pitch > arena_)
+        if (static_cast<size_t>(op.cols) * pitch * tiles > arena_ || static_cast<size_t>(op.rows) * pitch * tiles > arena_)
             return kFallback;
         Slab* slab = nullptr;
         for (;;) {
@@ -323,7 +338,7 @@ public:
                     if (s.state == Slab::kOpen) s.full = true;
                 for (Slab& s : slabs_)
                     if (s.state == Slab::kFree) {
-                        s.open(op, len, pitch, arena_, ++opened_);
+                        s.open(op, len, pitch, tiles, arena_, ++opened_);
                         slab = &s;
                         break;
                     }
@@ -338,14 +353,14 @@ public:
         if (slot == 0 || slab->full) cv_worker_.notify_one();
         lock.unlock();
 
-        const size_t in_stride = static_cast<size_t>(op.cols) * pitch;  // == the slab's (matches())
-        if (op.lens) {  // only the content bytes; the kernel reads the rest as zero
-            for (int j = 0; j < op.cols; ++j) {
-                slab->pin_lens[static_cast<size_t>(slot) * op.cols + j] = static_cast<uint32_t>(op.lens[j]);
-                if (op.lens[j]) std::memcpy(slab->pin_in + slot * in_stride + j * pitch, op.in[j], op.lens[j]);
-            }
-        } else {
-            for (int j = 0; j < op.cols; ++j) std::memcpy(slab->pin_in + slot * in_stride + j * pitch, op.in[j], len);
+        // tile t of column j at slot * in_stride + (t * cols + j) * pitch (untiled: t = 0)
+        const size_t in_stride = tiles * op.cols * pitch;  // == the slab's (matches())
+        uint8_t* const in_base = slab->pin_in + slot * in_stride;
+        for (int j = 0; j < op.cols; ++j) {
+            const size_t n = op.lens ? op.lens[j] : len;  // padded: only the content bytes
+            if (op.lens) slab->pin_lens[static_cast<size_t>(slot) * op.cols + j] = static_cast<uint32_t>(n);
+            for (size_t o = 0; o < n; o += pitch)  // untiled: pitch >= len, one copy
+                std::memcpy(in_base + (o / pitch * op.cols + j) * pitch, op.in[j] + o, std::min(pitch, n - o));
         }
 
         lock.lock();
@@ -355,9 +370,13 @@ public:
         lock.unlock();
 
         if (status == ELECT_EC_OK) {
-            const size_t out_stride = static_cast<size_t>(op.rows) * pitch;
+            const size_t out_stride = tiles * op.rows * pitch;
+            const uint8_t* const out_base = slab->pin_out + slot * out_stride;
             for (int r = 0; r < op.rows; ++r)
-                std::memcpy(op.out[r], slab->pin_out + slot * out_stride + r * pitch, len);
+                for (size_t t = 0; t < tiles; ++t) {
+                    const size_t o = t * pitch;
+                    std::memcpy(op.out[r] + o, out_base + (t * op.rows + r) * pitch, tiles > 1 ? std::min(pitch, len - o) : len);
+                }
             if (op.hashes)
                 std::memcpy(op.hashes, slab->pin_hash + static_cast<size_t>(slot) * op.rows, op.rows * sizeof(int32_t));
         }
@@ -372,7 +391,7 @@ public:
 private:
     struct Shape {  // what a batch computes, copied out of its slab under mu_
         int cols = 0, rows = 0;
-        size_t len = 0, pitch = 0;
+        size_t len = 0, pitch = 0, tiles = 1;
         bool padded = false, hashed = false;
         uint8_t coef[kern::kMaxRows * kern::kMaxCols] = {};
     };
@@ -381,7 +400,7 @@ private:
         enum State { kFree, kOpen, kInFlight, kDone } state = kFree;
         Batcher* owner = nullptr;
         int cols = 0, rows = 0;
-        size_t len = 0, pitch = 0;
+        size_t len = 0, pitch = 0, tiles = 1;
         uint8_t coef[kern::kMaxRows * kern::kMaxCols] = {};
         int capacity = 0, reserved = 0, filled = 0, readers = 0, status = ELECT_EC_OK;
         bool full = false;
@@ -404,6 +423,7 @@ private:
             sh.rows = rows;
             sh.len = len;
             sh.pitch = pitch;
+            sh.tiles = tiles;
             sh.padded = padded;
             sh.hashed = hashed;
             std::memcpy(sh.coef, coef, sizeof(coef));
@@ -416,16 +436,17 @@ private:
                    (op.hashes != nullptr) == hashed && std::memcmp(op.coef, coef, sizeof(coef)) == 0;
         }
 
-        void open(const HostOp& op, size_t n, size_t p, size_t arena, uint64_t order)
+        void open(const HostOp& op, size_t n, size_t p, size_t t, size_t arena, uint64_t order)
         {
             cols = op.cols;
             rows = op.rows;
             len = n;
             pitch = p;
+            tiles = t;
             std::memcpy(coef, op.coef, sizeof(coef));
             padded = op.lens != nullptr;
             hashed = op.hashes != nullptr;
-            size_t cap = arena / (static_cast<size_t>(std::max(cols, rows)) * pitch);
+            size_t cap = arena / (static_cast<size_t>(std::max(cols, rows)) * pitch * tiles);
             if (padded) cap = std::min(cap, kMetaEntries / cols);
             if (hashed) cap = std::min(cap, kMetaEntries / rows);
             capacity = static_cast<int>(cap);
@@ -445,10 +466,11 @@ private:
             s.owner = this;
             hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming);
-            if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_in), arena, hipHostMallocDefault);
-            if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_out), arena, hipHostMallocDefault);
+            // device first: an arena too large for the device fails there, before any host pinning
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_in), arena);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_out), arena);
+            if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_in), arena, hipHostMallocDefault);
+            if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_out), arena, hipHostMallocDefault);
             const size_t meta = kMetaEntries * sizeof(uint32_t);
             if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_lens), meta, hipHostMallocDefault);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_lens), meta);
@@ -459,6 +481,29 @@ private:
             if (e != hipSuccess) return map_hip(e);
         }
         return ELECT_EC_OK;
+    }
+
+    // Frees whatever init() allocated (after a failed init: nothing is in flight).
+    void release()
+    {
+        for (Slab& s : slabs_) {
+            if (s.stream) (void)hipStreamDestroy(s.stream);
+            if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
+            for (uint8_t* h : {s.pin_in, s.pin_out})
+                if (h) (void)hipHostFree(h);
+            for (void* h : {static_cast<void*>(s.pin_lens), static_cast<void*>(s.pin_hash)})
+                if (h) (void)hipHostFree(h);
+            for (void* d : {static_cast<void*>(s.d_in), static_cast<void*>(s.d_out), static_cast<void*>(s.d_lens),
+                            static_cast<void*>(s.d_hash), static_cast<void*>(s.d_scratch)})
+                if (d) (void)hipFree(d);
+            s.stream = nullptr;
+            s.h2d_done = nullptr;
+            s.pin_in = s.pin_out = s.d_in = s.d_out = nullptr;
+            s.pin_lens = s.d_lens = nullptr;
+            s.pin_hash = s.d_hash = nullptr;
+            s.d_scratch = nullptr;
+        }
+        arena_ = 0;
     }
 
     // Self-clocking dispatch: a batch leaves as soon as the previous batch's
@@ -506,22 +551,29 @@ private:
     // read from the copy taken under mu_.
     static hipError_t issue(Slab& s, const Shape& sh, int n)
     {
-        const size_t in_stride = static_cast<size_t>(sh.cols) * sh.pitch;
-        const size_t out_stride = static_cast<size_t>(sh.rows) * sh.pitch;
+        const size_t in_stride = sh.tiles * sh.cols * sh.pitch;  // per slot
+        const size_t out_stride = sh.tiles * sh.rows * sh.pitch;
         hipError_t e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
         if (e == hipSuccess && sh.padded)
             e = hipMemcpyAsync(s.d_lens, s.pin_lens, static_cast<size_t>(n) * sh.cols * sizeof(uint32_t),
                                hipMemcpyHostToDevice, s.stream);
         if (e == hipSuccess) e = hipEventRecord(s.h2d_done, s.stream);
         if (e == hipSuccess) {
+            // coding stripes: the slots' tiles in order (untiled: the slots)
             ApplyParams p;
-            p.len = sh.len;
-            p.stripes = static_cast<uint64_t>(n);
+            p.len = sh.tiles > 1 ? sh.pitch : sh.len;
+            p.stripes = static_cast<uint64_t>(n) * sh.tiles;
             p.cols = sh.cols;
             p.rows = sh.rows;
-            for (int j = 0; j < sh.cols; ++j) p.src[j] = col(s.d_in, in_stride, j * sh.pitch);
-            for (int r = 0; r < sh.rows; ++r) p.dst[r] = col(s.d_out, out_stride, r * sh.pitch);
+            for (int j = 0; j < sh.cols; ++j) p.src[j] = col(s.d_in, sh.cols * sh.pitch, j * sh.pitch);
+            for (int r = 0; r < sh.rows; ++r) p.dst[r] = col(s.d_out, sh.rows * sh.pitch, r * sh.pitch);
             std::memcpy(p.coef, sh.coef, sizeof(p.coef));
+            if (sh.tiles > 1) {
+                p.tiles = static_cast<uint32_t>(sh.tiles);
+                p.unit_len = sh.len;
+                p.padded = true;
+                for (int j = 0; j < sh.cols; ++j) p.clen[j] = static_cast<uint32_t>(sh.len);
+            }
             if (sh.padded) {
                 p.padded = true;
                 p.lens = s.d_lens;
@@ -570,6 +622,7 @@ private:
     std::condition_variable cv_worker_;  // the dispatcher
     std::condition_variable cv_slot_;    // callers waiting for an arena to reserve in
     bool started_ = false;
+    bool init_failed_ = false;  // the arenas could not be allocated: every call runs directly
     size_t arena_ = 0;
     uint64_t opened_ = 0;
     Slab slabs_[kSlabs];

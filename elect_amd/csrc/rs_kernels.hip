@@ -267,7 +267,12 @@ struct FastArgs {
     uint32_t lstride;
     uint32_t lcols;          // columns >= lcols hold clen[j] valid bytes
     uint32_t clen[K];
-    int32_t* hashes;        // optional parity hashes, [stripe][hstride] (row r at +r)
+    uint32_t ulen32;         // min(logical unit length, 2^32-1): content lengths clamp to it
+    uint32_t tiles;          // coding stripes (tiles) per logical stripe, 1 = untiled
+    uint32_t tmagic, tshift; // exact division by tiles
+    uint32_t hsegs;          // segments per hashed (logical) unit: tiles * segs
+    uint32_t hmagic, hshift; // exact division by hsegs
+    int32_t* hashes;        // optional parity hashes, [logical stripe][hstride] (row r at +r)
     uint32_t hstride;
     uint32_t hpow;          // 31^(hash offset of byte 0 of this launch window)
     uint32_t* hpart;        // per-wave partial sums [wave][R]: the wave's first stripe
@@ -276,6 +281,37 @@ struct FastArgs {
 };
 
 constexpr int kTabStride = 8;  // dwords per coefficient in LDS
+
+__device__ __forceinline__ uint32_t div_magic(uint32_t n, uint32_t m, uint32_t sh)
+{
+    return static_cast<uint32_t>((static_cast<uint64_t>(n) * m) >> sh);
+}
+
+// Valid bytes of one tile (offset tb in its unit, tl bytes long) of a unit
+// holding `raw` content bytes.  Untiled: tb = 0 and raw <= tl, so raw itself.
+__device__ __forceinline__ uint32_t tile_valid(uint32_t raw, uint32_t tb, uint32_t tl)
+{
+    return raw > tb ? min(raw - tb, tl) : 0u;
+}
+
+// Content bytes of column j of coding stripe `stripe` (its logical stripe's
+// length from lens, or clen), as the tile's share.
+template <int K, typename A>
+__device__ __forceinline__ void tile_lengths(const A& a, uint32_t stripe, uint32_t (&valid)[K], bool scalar)
+{
+    const uint32_t g = div_magic(stripe, a.tmagic, a.tshift);
+    const uint32_t tb = (stripe - g * a.tiles) * a.len32;
+    const uint32_t* l = a.lens ? a.lens + static_cast<uint64_t>(g) * a.lstride : nullptr;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        uint32_t raw = a.clen[j];
+        if (l && j < static_cast<int>(a.lcols)) {
+            const uint32_t v = scalar ? static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(l[j])) : l[j];
+            raw = min(v, a.ulen32);
+        }
+        valid[j] = tile_valid(raw, tb, a.len32);
+    }
+}
 
 // cmask (wave-uniform): columns to include; the others are known zero for the
 // whole wave and are skipped by a scalar branch (padded launches).
@@ -412,12 +448,10 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
     uint32_t sl[K];
     const uint32_t first = __builtin_amdgcn_readfirstlane(idx_raw);
     if (PAD && a.lens && first < a.total) {  // (a wholly dead wave reads nothing)
-        const uint32_t s0 = static_cast<uint32_t>((static_cast<uint64_t>(first) * a.magic) >> a.shift);
-        const uint32_t s1 = static_cast<uint32_t>((static_cast<uint64_t>(first + 63) * a.magic) >> a.shift);
+        const uint32_t s0 = div_magic(first, a.magic, a.shift);
+        const uint32_t s1 = div_magic(first + 63, a.magic, a.shift);
         uniform = s0 == s1;
-        const uint32_t* l = a.lens + static_cast<uint64_t>(s0) * a.lstride;
-#pragma unroll
-        for (int j = 0; j < K; ++j) sl[j] = j < a.lcols ? min(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(l[j])), a.len32) : a.clen[j];
+        tile_lengths<K>(a, s0, sl, true);
     }
 
     stage_tables(a, tl);
@@ -429,16 +463,11 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 
     if (PAD) {
         uint32_t valid[K];
-        if (!a.lens) {
-#pragma unroll
-            for (int j = 0; j < K; ++j) valid[j] = a.clen[j];
-        } else if (uniform) {
+        if (a.lens && uniform) {
 #pragma unroll
             for (int j = 0; j < K; ++j) valid[j] = sl[j];
         } else {  // all lengths first: vmcnt is in order, so interleaving would serialise
-            const uint32_t* l = a.lens + static_cast<uint64_t>(stripe) * a.lstride;
-#pragma unroll
-            for (int j = 0; j < K; ++j) valid[j] = j < a.lcols ? min(l[j], a.len32) : a.clen[j];
+            tile_lengths<K>(a, stripe, valid, false);
         }
         // Full segments first (no loads at all past a column's content length),
         // then the one segment per unit that holds the content end, loaded whole
@@ -487,12 +516,16 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
                     set_word(acc[r], w, lane_word(acc[r], w) & keep);
                 }
         }
+        // Hashed units are logical stripes (tiles of one unit are consecutive
+        // coding stripes): position = flat index - the unit's first segment.
         const uint32_t last = first + 63;
-        const uint32_t s_first = static_cast<uint32_t>((static_cast<uint64_t>(first) * a.magic) >> a.shift);
-        const uint32_t s_last = static_cast<uint32_t>((static_cast<uint64_t>(last) * a.magic) >> a.shift);
+        const uint32_t s_first = div_magic(first, a.hmagic, a.hshift);
+        const uint32_t s_last = div_magic(last, a.hmagic, a.hshift);
         const bool whole_wave = last < a.total && s_first == s_last;  // wave-uniform
+        const uint32_t hs = div_magic(idx, a.hmagic, a.hshift);       // this lane's hashed unit
+        const uint32_t hseg = idx - hs * a.hsegs;                     // its segment inside it
         if (whole_wave) {  // partial sums to scratch; hash_reduce adds them per stripe
-            const uint32_t seg0 = first - s_first * a.segs;
+            const uint32_t seg0 = first - s_first * a.hsegs;
             const uint32_t p0 = a.hpow * pow31_seg(seg0);
             const uint32_t q = kLanePow.v[threadIdx.x & 63u] * p0;
 #pragma unroll
@@ -501,8 +534,8 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
                 if ((threadIdx.x & 63u) == 0) a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum;
             }
         } else if (a.hpart_hi) {  // assign mode: a wave straddling two stripes (or the launch's end)
-            const uint32_t p = live ? a.hpow * pow31_seg(static_cast<uint32_t>(off >> 4)) : 0u;
-            const bool lo = stripe == s_first;
+            const uint32_t p = live ? a.hpow * pow31_seg(hseg) : 0u;
+            const bool lo = hs == s_first;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const uint32_t v = horner31(acc[r]) * p;
@@ -514,10 +547,10 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
                 }
             }
         } else if (live) {
-            const uint32_t p = a.hpow * pow31_seg(static_cast<uint32_t>(off >> 4));
+            const uint32_t p = a.hpow * pow31_seg(hseg);
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                atomicAdd(reinterpret_cast<unsigned*>(a.hashes) + static_cast<uint64_t>(stripe) * a.hstride + r,
+                atomicAdd(reinterpret_cast<unsigned*>(a.hashes) + static_cast<uint64_t>(hs) * a.hstride + r,
                           horner31(acc[r]) * p);
         }
     }
@@ -545,9 +578,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
     if (first < a.total) {
         s0 = stripe_of(first);
         uniform = s0 == stripe_of(min(first + 64u * U - 1u, a.total - 1u));
-        const uint32_t* l = a.lens + static_cast<uint64_t>(s0) * a.lstride;
-#pragma unroll
-        for (int j = 0; j < K; ++j) sl[j] = j < a.lcols ? min(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(l[j])), a.len32) : a.clen[j];
+        tile_lengths<K>(a, s0, sl, true);
     }
     stage_tables(a, tl);
     if (first >= a.total) return;
@@ -605,10 +636,8 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
         if (idx >= a.total) break;
         const uint32_t stripe = stripe_of(idx);
         const uint64_t off = static_cast<uint64_t>(idx - stripe * a.segs) * 16;
-        const uint32_t* l = a.lens + static_cast<uint64_t>(stripe) * a.lstride;
         uint32_t valid[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) valid[j] = j < a.lcols ? min(l[j], a.len32) : a.clen[j];
+        tile_lengths<K>(a, stripe, valid, false);
         uint4 x[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
@@ -778,6 +807,18 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     a.shift = mg.p;
     a.len = p.len;
     a.len32 = static_cast<uint32_t>(std::min<uint64_t>(p.len, 0xFFFFFFFFu));
+    const uint32_t tiles = std::max<uint32_t>(1, p.tiles);
+    const uint64_t ulen = p.unit_len ? p.unit_len : p.len;
+    a.ulen32 = static_cast<uint32_t>(std::min<uint64_t>(ulen, 0xFFFFFFFFu));
+    a.tiles = tiles;
+    const Magic tm = make_magic(tiles);
+    a.tmagic = tm.m;
+    a.tshift = tm.p;
+    if (segs64 * tiles > kMaxIndex) return hipErrorInvalidValue;
+    a.hsegs = static_cast<uint32_t>(segs64 * tiles);
+    const Magic hm = make_magic(a.hsegs);
+    a.hmagic = hm.m;
+    a.hshift = hm.p;
     a.lstride = p.lens_stride ? p.lens_stride : static_cast<uint32_t>(p.cols);
     a.lcols = static_cast<uint32_t>(p.lens_cols ? p.lens_cols : p.cols);
     for (int j = 0; j < K; ++j) a.clen[j] = p.clen[j];
@@ -787,7 +828,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(p.coef[(r0 + r) * p.cols + j]);
     const int block = block_for(p.len, R * K);
     const bool hash_assign = p.hashes && p.hash_seed;  // launch_apply chose assign mode
-    const uint64_t per_launch = kMaxIndex / segs64;  // stripes per launch keeping idx < 2^31
+    // stripes per launch keeping idx < 2^31, whole logical stripes (tiles) per launch
+    const uint64_t per_launch = kMaxIndex / segs64 / tiles * tiles;
     for (uint64_t s0 = 0; s0 < p.stripes; s0 += per_launch) {
         const uint64_t ns = std::min<uint64_t>(per_launch, p.stripes - s0);
         for (int j = 0; j < K; ++j) {
@@ -798,8 +840,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             a.dp[r] = const_cast<uint8_t*>(p.dst[r0 + r].ptr) + s0 * p.dst[r0 + r].stride;
             a.ds[r] = p.dst[r0 + r].stride;
         }
-        a.lens = p.lens ? p.lens + s0 * a.lstride : nullptr;
-        a.hashes = p.hashes ? p.hashes + s0 * p.hash_stride + r0 : nullptr;
+        a.lens = p.lens ? p.lens + s0 / tiles * a.lstride : nullptr;
+        a.hashes = p.hashes ? p.hashes + s0 / tiles * p.hash_stride + r0 : nullptr;
         a.total = static_cast<uint32_t>(ns * segs64);
         a.hpart = nullptr;
         a.hpart_hi = nullptr;
@@ -811,7 +853,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         }
         bool lens_path = false;
         if constexpr (PAD) {
-            lens_path = a.lens && !a.hashes && p.aligned16 && p.len % 16 == 0 && p.len < (uint64_t{1} << 31);
+            lens_path = (a.lens || tiles > 1) && !a.hashes && p.aligned16 && p.len % 16 == 0 &&
+                        p.len < (uint64_t{1} << 31);
 #ifdef AB_NO_LENS
             lens_path = false;
 #endif
@@ -832,9 +875,10 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         }
         hipError_t e = hipGetLastError();
         if (e == hipSuccess && a.hashes) {
-            const uint32_t n = static_cast<uint32_t>(ns) * R;  // one wave each
+            const uint32_t units = static_cast<uint32_t>(ns / tiles);
+            const uint32_t n = units * R;  // one wave each
             hipLaunchKernelGGL(hash_reduce, dim3((n + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, stream, a.hpart,
-                               a.hpart_hi, a.hashes, a.hstride, R, a.segs, static_cast<uint32_t>(ns), pow31(p.len));
+                               a.hpart_hi, a.hashes, a.hstride, R, a.hsegs, units, pow31(ulen));
             e = hipGetLastError();
         }
         if (e != hipSuccess) return e;
@@ -1159,14 +1203,19 @@ hipError_t launch_apply_impl(const ApplyParams& p_in, hipStream_t stream)
     if (p.hashes && p.cols > kMaxHashCols) return hipErrorInvalidValue;  // hashes are an encode feature
     p.aligned16 = apply_is_aligned(p);
     const bool vec = p.aligned16 || unaligned_vector_ok();  // dwordx4 kernels usable
+    const uint32_t tiles = std::max<uint32_t>(1, p.tiles);
+    const uint64_t ulen = p.unit_len ? p.unit_len : p.len;
+    if (tiles > 1 && (!p.padded || p.len == 0 || p.len % 16 || p.stripes % tiles || ulen > tiles * p.len ||
+                      !vec || p.cols > kMaxPadCols))
+        return hipErrorInvalidValue;  // tiling rides on the padded vector kernels only
     if (p.hashes && p.hash_seed) {
-        // Assign mode needs the fast kernel with >= 64 segments per stripe (every
-        // wave within two stripes); anything else seeds the entries and adds.
+        // Assign mode needs the fast kernel with >= 64 segments per hashed unit
+        // (every wave within two units); anything else seeds the entries and adds.
         const bool fast = vec && (!p.padded || p.cols <= kMaxPadCols);
-        const uint64_t segs = p.padded ? (p.len + 15) / 16 : p.len / 16;
+        const uint64_t segs = (p.padded ? (p.len + 15) / 16 : p.len / 16) * tiles;
         if (!fast || segs < 64) {
-            const hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.hashes),
-                                                   static_cast<int>(pow31(p.len)), p.stripes * p.hash_stride, stream);
+            const hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.hashes), static_cast<int>(pow31(ulen)),
+                                                   p.stripes / tiles * p.hash_stride, stream);
             if (e != hipSuccess) return e;
             p.hash_seed = false;
         }
@@ -1174,7 +1223,7 @@ hipError_t launch_apply_impl(const ApplyParams& p_in, hipStream_t stream)
     if (p.len == 0) return hipSuccess;
     if (p.padded) {
         for (int j = 0; j < p.cols; ++j)
-            if ((!p.lens || (p.lens_cols && j >= p.lens_cols)) && p.clen[j] > p.len) return hipErrorInvalidValue;
+            if ((!p.lens || (p.lens_cols && j >= p.lens_cols)) && p.clen[j] > ulen) return hipErrorInvalidValue;
         if (!vec || p.cols > kMaxPadCols) return launch_bytes(p, stream);
         for (int r0 = 0; r0 < p.rows; r0 += kFastRows) {
             const int nr = std::min(kFastRows, p.rows - r0);

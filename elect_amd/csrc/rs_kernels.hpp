@@ -71,6 +71,16 @@ struct ApplyParams {
     // it launch_apply leases the stream's cached buffer.
     uint32_t* hash_scratch = nullptr;
     size_t hash_scratch_words = 0;
+    // Tiled units: each logical unit of unit_len bytes is stored as `tiles`
+    // tiles of len bytes, tile t of logical stripe g being coding stripe
+    // g * tiles + t (so `stripes` counts tiles, a multiple of `tiles`).  The
+    // content lengths (lens, clen) and the hashes are per LOGICAL unit; a tile
+    // holds its share of its unit's content and the bytes past unit_len are
+    // never read (they code as zero).  Units of any length can then be coded
+    // as 64 KiB units back to back, the layout HBM streams best.
+    // Needs padded, len % 16 == 0 and the vector kernels.
+    uint32_t tiles = 1;
+    uint64_t unit_len = 0;  // 0: len (untiled)
     // internal (launch_apply): every column start is 16-byte aligned.  When it
     // is not, the dwordx4 kernels still run (unaligned vector access, see
     // unaligned_vector_ok) except gf_apply_lens, whose buffer loads need it.

@@ -244,6 +244,31 @@ int elect_ec_decode_batch_ex(const elect_ec_coder* coder, size_t chunk_size, siz
                              elect_ec_shards inputs, const uint32_t* d_input_lengths, const int* decode_indexes,
                              const int* erased_indexes, int num_erased, elect_ec_shards outputs,
                              unsigned flags, int mode, void* stream);
+/* ---- device resident, tiled units ----
+ * The three _ex calls with every unit of chunk_size bytes stored as
+ * T = ceil(chunk_size / tile_bytes) tiles of tile_bytes bytes (a multiple of
+ * 16; 65536 is the unit size HBM streams best, DESIGN.md §3, so ELECT's
+ * codeLength of 4,404,020 B runs as 68 tiles at the 64 KiB rate).  The shard
+ * descriptors address TILES: tile t of unit j of stripe s starts at
+ *   base + (s*T + t) * stripe_stride + j * shard_stride
+ * (a [B][T][k+m][tile] block: stripe_stride = (k+m)*tile, shard_stride = tile).
+ * Content lengths (NULL = all chunk_size) and hashes are per STRIPE exactly as
+ * in the _ex calls, and the bytes produced are those of coding each unit whole:
+ * bytes of a unit's last tile past chunk_size are never read, and the outputs
+ * there are written as zero.  Needs the vector kernels (16-byte aligned bases
+ * and strides, or elect_ec_unaligned_vector_ok) and at most 10 columns. */
+int elect_ec_encode_batch_tiled(const elect_ec_coder* coder, size_t chunk_size, size_t tile_bytes,
+                                size_t num_stripes, elect_ec_shards data, const uint32_t* d_data_lengths,
+                                elect_ec_shards parity, int32_t* d_hashes, void* stream);
+int elect_ec_encode_update_batch_tiled(const elect_ec_coder* coder, size_t chunk_size, size_t tile_bytes,
+                                       size_t num_stripes, int target_data_index, elect_ec_column old_data,
+                                       elect_ec_column new_data, const uint32_t* d_old_new_lengths,
+                                       elect_ec_shards parity_in, elect_ec_shards parity_out, int32_t* d_hashes,
+                                       void* stream);
+int elect_ec_decode_batch_tiled(const elect_ec_coder* coder, size_t chunk_size, size_t tile_bytes,
+                                size_t num_stripes, elect_ec_shards inputs, const uint32_t* d_input_lengths,
+                                const int* decode_indexes, const int* erased_indexes, int num_erased,
+                                elect_ec_shards outputs, unsigned flags, int mode, void* stream);
 /* General product dst[r] = XOR_j coef[r*cols+j] * src[j], rows, cols <= 16. */
 int elect_ec_apply_batch(const unsigned char* coef, int rows, int cols, size_t chunk_size,
                          size_t num_stripes, const elect_ec_column* src,

@@ -620,3 +620,32 @@ def test_tiled_layout_equals_contiguous(dev):
     torch.cuda.synchronize()
     assert torch.equal(tiled[:, :, k:].transpose(1, 2).reshape(B, m, L), flat[:, k:])
     assert torch.equal(out.view(B, L), flat[:, 0])
+
+
+def test_batcher_arena_failure_falls_back(dev, tmp_path):
+    """ELECT_EC_BATCH_ARENA_MB far beyond what can be pinned: the batcher's arena
+    allocation fails, it frees what it got and every host call runs on the
+    per-thread engine instead of failing (and keeps doing so)."""
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    code = f"""
+import sys, numpy as np
+sys.path.insert(0, {ROOT!r})
+from elect_amd.coder import RSCoder
+from oracle import ec_oracle
+k, m = 4, 2
+c = RSCoder(k, m)
+for L in (4404020, 4099, 65536 * 3):
+    for it in range(2):
+        rng = np.random.default_rng(L + it)
+        d = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+        p = [np.empty(L, np.uint8) for _ in range(m)]
+        c.encode_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L)
+        want = ec_oracle.Encoder(k, m).encode(d)
+        assert all(np.array_equal(a, b) for a, b in zip(p, want)), L
+print("fallback ok")
+"""
+    env = dict(__import__("os").environ, ELECT_EC_BATCH_ARENA_MB=str(64 << 20))  # 64 TiB per arena
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0 and "fallback ok" in r.stdout, r.stdout + r.stderr

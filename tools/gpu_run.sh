@@ -74,9 +74,13 @@ for step in "$@"; do
     hashed)
         run bench_hashed 400 python bench.py --config hashed || exit $?
         run bench_hashed_1M 400 python bench.py --config hashed --chunk 1048576 || exit $? ;;
-    flows)  # ELECT's two coding-node steps, fused (padded + hashed encode, padded + hashed update)
+    flows)  # ELECT's three coding-node steps, fused; ELECT's codeLength tiled (default) and untiled
         run bench_flows 400 python bench.py --config flows || exit $?
-        run bench_flows_elect 400 python bench.py --config flows --chunk 4404020 --stripes 256 || exit $? ;;
+        run bench_flows_elect 400 python bench.py --config flows --chunk 4404020 --stripes 256 || exit $?
+        run bench_flows_elect_untiled 400 python bench.py --config flows --chunk 4404020 --stripes 256 --flows-tile 0 || exit $? ;;
+    gputests)  # a subset: GPU_TESTS="tests/test_gpu_tiled.py ..."
+        run pytest_gpu_subset 900 python -m pytest ${GPU_TESTS} -m gpu -x -q -p no:cacheprovider --timeout 300
+        rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     hostsweep) run hostsweep 600 python tools/tune/host_sweep.py || exit $? ;;
     copysizes) run copysizes 600 python tools/tune/host_sweep.py copysizes || exit $? ;;
     staged)
