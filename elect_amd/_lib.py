@@ -78,6 +78,7 @@ SIGNATURES = [
     ("elect_ec_coder_encode_matrix", ctypes.c_int, [_cp, _u8p, ctypes.c_size_t]),
     ("elect_ec_coder_gf_tables", ctypes.c_int, [_cp, _u8p, ctypes.c_size_t]),
     ("elect_ec_coder_decode_matrix", ctypes.c_int, [_cp, _ip, _ip, ctypes.c_int, ctypes.c_int, _u8p]),
+    ("elect_ec_coder_invert_matrix", ctypes.c_int, [_cp, _ip, _u8p]),
     ("elect_ec_encode", ctypes.c_int, [_cp, _u8pp, _u8pp, ctypes.c_size_t]),
     ("elect_ec_encode_update", ctypes.c_int, [_cp, _u8pp, ctypes.c_int, _u8pp, ctypes.c_size_t]),
     ("elect_ec_encode_padded", ctypes.c_int, [_cp, _u8pp, ctypes.POINTER(ctypes.c_size_t), _u8pp,

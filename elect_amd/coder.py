@@ -236,6 +236,13 @@ class RSCoder:
                                                     out.ctypes.data_as(_lib._u8p)), "decode matrix")
         return st, out[: len(erased) * self.k].reshape(len(erased), self.k)
 
+    def invert_matrix(self, decode_indexes):
+        """(status, k x k inverse of the survivor rows); WARN_SINGULAR with the partial state."""
+        out = np.zeros(self.k * self.k, np.uint8)
+        st = check(lib.elect_ec_coder_invert_matrix(self.handle, int_array(decode_indexes),
+                                                    out.ctypes.data_as(_lib._u8p)), "invert matrix")
+        return st, out.reshape(self.k, self.k)
+
     # host-memory, synchronous (the JNI calling convention)
     def encode_host(self, data_addrs, parity_addrs, length: int) -> int:
         return check(lib.elect_ec_encode(self.handle, ptr_array(data_addrs), ptr_array(parity_addrs),

@@ -181,7 +181,7 @@ int update_batch_impl(const elect_ec_coder* coder, size_t chunk_size, size_t til
                       int32_t* d_hashes, void* stream)
 {
     if (!valid_coder(coder) || target_data_index < 0 || target_data_index >= coder->k) return ELECT_EC_EINVAL;
-    if (d_hashes && 2 + coder->m > ELECT_EC_MAX_DATA_UNITS) return ELECT_EC_EINVAL;
+    if (d_hashes && tile && 2 + coder->m > ELECT_EC_MAX_DATA_UNITS) return ELECT_EC_EINVAL;
     if ((d_old_new_lengths || tile) && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
     if (num_stripes == 0 || (chunk_size == 0 && !d_hashes)) return ELECT_EC_OK;
     if (chunk_size > 0 && (!old_data.ptr || !new_data.ptr || !parity_in.base || !parity_out.base))
@@ -306,6 +306,17 @@ int elect_ec_coder_gf_tables(const elect_ec_coder* coder, unsigned char* out, si
     return ELECT_EC_OK;
 }
 
+int elect_ec_coder_invert_matrix(const elect_ec_coder* coder, const int* decode_indexes, unsigned char* out)
+{
+    if (!valid_coder(coder) || !decode_indexes || !out) return ELECT_EC_EINVAL;
+    const int k = coder->k;
+    for (int j = 0; j < k; ++j)
+        if (decode_indexes[j] < 0 || decode_indexes[j] >= k + coder->m) return ELECT_EC_EINVAL;
+    uint8_t work[ELECT_EC_MAX_DATA_UNITS * ELECT_EC_MAX_DATA_UNITS];
+    for (int i = 0; i < k; ++i) std::memcpy(work + i * k, coder->gen + decode_indexes[i] * k, k);
+    return elect::gf::invert(work, out, k) ? ELECT_EC_OK : ELECT_EC_WARN_SINGULAR;
+}
+
 int elect_ec_coder_decode_matrix(const elect_ec_coder* coder, const int* decode_indexes,
                                  const int* erased_indexes, int num_erased, int mode, unsigned char* out)
 {
@@ -376,7 +387,6 @@ int elect_ec_encode_update_ex(const elect_ec_coder* coder, const unsigned char* 
 {
     if (!valid_coder(coder) || !old_new_parity || !new_parity_units) return ELECT_EC_EINVAL;
     if (target_data_index < 0 || target_data_index >= coder->k) return ELECT_EC_EINVAL;
-    if (hashes && 2 + coder->m > ELECT_EC_MAX_DATA_UNITS) return ELECT_EC_EINVAL;
     if (old_new_lengths && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
     if (hashes && chunk_size == 0) {
         for (int r = 0; r < coder->m; ++r) hashes[r] = 1;

@@ -283,6 +283,7 @@ struct BatchConfig {
     std::atomic<int> enabled{-1};  // -1: read ELECT_EC_BATCH on first use
     std::atomic<unsigned> window_us{0};
     std::atomic<size_t> arena_bytes{size_t{256} << 20};
+    std::atomic<size_t> tile{size_t{1} << 16};  // ELECT_EC_BATCH_TILE_KB (0: untiled arena)
 };
 
 BatchConfig& batch_config()
@@ -292,8 +293,10 @@ BatchConfig& batch_config()
         const char* e = std::getenv("ELECT_EC_BATCH");
         const char* w = std::getenv("ELECT_EC_BATCH_WINDOW_US");
         const char* a = std::getenv("ELECT_EC_BATCH_ARENA_MB");
+        const char* t = std::getenv("ELECT_EC_BATCH_TILE_KB");
         if (w) c.window_us = static_cast<unsigned>(std::atoi(w));
-        if (a && std::atoi(a) > 0) c.arena_bytes = static_cast<size_t>(std::atoi(a)) << 20;
+        if (a && std::atoll(a) > 0) c.arena_bytes = static_cast<size_t>(std::atoll(a)) << 20;
+        if (t && std::atoi(t) >= 0) c.tile = static_cast<size_t>(std::atoi(t)) << 10;
         int expect = -1;
         c.enabled.compare_exchange_strong(expect, (!e || std::atoi(e) > 0) ? 1 : 0);  // on unless ELECT_EC_BATCH=0
     }
@@ -304,7 +307,6 @@ class Batcher {
 public:
     static constexpr int kFallback = 1000;  // request does not fit (or no arena): run it directly
     static constexpr int kSlabs = 2;
-    static constexpr size_t kTile = size_t{1} << 16;
     // Per-slot content lengths (padded ops) and parity hashes (hashed ops) of a
     // batch: entries per arena, which caps such a batch's stripes.
     static constexpr size_t kMetaEntries = size_t{1} << 16;
@@ -314,8 +316,9 @@ public:
     int submit(const HostOp& op, size_t len)
     {
         // untiled: one unit per column at a 256-byte pitch; tiled: T tiles of 64 KiB
-        const size_t tiles = len > kTile ? (len + kTile - 1) / kTile : 1;
-        const size_t pitch = tiles > 1 ? kTile : (len + 255) & ~size_t{255};
+        const size_t tile = batch_config().tile.load();
+        const size_t tiles = tile && tile % 16 == 0 && len > tile ? (len + tile - 1) / tile : 1;
+        const size_t pitch = tiles > 1 ? tile : (len + 255) & ~size_t{255};
         std::unique_lock<std::mutex> lock(mu_);
         if (init_failed_) return kFallback;
         if (!started_) {  // arenas, streams and events once, before anything is in flight

@@ -13,11 +13,19 @@
  *
  * Differences from the reference glue, all on error paths:
  *  - every THROW returns (EC/NativeRSDecoder.c:50-52 and EC/jni_common.c:70-73,
- *    95-97 fall through after throwing);
+ *    95-97 fall through after throwing), and no JNI call but the exception-safe
+ *    ones runs while an exception is pending (ExceptionCheck first);
  *  - int arrays are released (EC/jni_common.c:75, 99 and EC/NativeRSDecoder.c:59-62 leak);
  *  - a negative engine status becomes a Java exception instead of being ignored;
+ *  - a negative dataLen is an IllegalArgumentException (the reference memsets a
+ *    negative size: EC/erasure_coder.c:86-88);
  *  - the three unconditional printf lines of decodeImpl (EC/NativeRSDecoder.c:57,
  *    65, 68) print only when allowVerboseDump() is true.
+ * With allowVerboseDump() true (read on every call, EC/jni_common.c:44-57) the
+ * coder dumps print in EC/dump.c's format: the encoder block (dumpEncoder,
+ * EC/dump.c:61-73) on encode/encodeUpdate, the decoder block (dumpDecoder,
+ * :75-104: erased and decode indexes, encode / invert / decode matrices) on
+ * decode after the reference's three decodeImpl lines.
  *
  * JEC/ = src/elect/src/java/org/apache/cassandra/io/erasurecode
  * EC/  = src/elect/src/native/src/org/apache/cassandra/io/erasurecode
@@ -63,6 +71,8 @@ static jfieldID coder_field(JNIEnv* env, jobject thiz)
     return fid;
 }
 
+/* allowVerboseDump() (EC/jni_common.c:44-50): 1 / 0, or -1 when the call threw
+ * (the exception stays pending for the caller to return with). */
 static int verbose(JNIEnv* env, jobject thiz)
 {
     jclass clazz = (*env)->GetObjectClass(env, thiz);
@@ -71,16 +81,90 @@ static int verbose(JNIEnv* env, jobject thiz)
         (*env)->ExceptionClear(env);
         return 0;
     }
-    return (*env)->CallBooleanMethod(env, thiz, mid) == JNI_TRUE;
+    jboolean v = (*env)->CallBooleanMethod(env, thiz, mid);
+    if ((*env)->ExceptionCheck(env))
+        return -1;
+    return v == JNI_TRUE;
 }
 
-/* getCoder, EC/jni_common.c:35-60 */
+/* getCoder, EC/jni_common.c:35-60.  NULL with an exception pending when the
+ * field is missing; NULL with none when the coder was released. */
 static elect_ec_coder* get_coder(JNIEnv* env, jobject thiz)
 {
     jfieldID fid = coder_field(env, thiz);
     if (fid == NULL)
         return NULL;
     return (elect_ec_coder*)(intptr_t)(*env)->GetLongField(env, thiz, fid);
+}
+
+/* The coder of a coding call, or NULL after raising: closed coder -> IOException
+ * (EC/NativeRSEncoder.c:49-51); a pending exception is left as it is. */
+static elect_ec_coder* coder_for_call(JNIEnv* env, jobject thiz, const char* closed_msg)
+{
+    elect_ec_coder* c = get_coder(env, thiz);
+    if (c == NULL && !(*env)->ExceptionCheck(env))
+        throw_java(env, "java/io/IOException", closed_msg);
+    return c;
+}
+
+static int bad_length(JNIEnv* env, jint dataLen)
+{
+    if (dataLen >= 0)
+        return 0;
+    throw_java(env, "java/lang/IllegalArgumentException", "negative dataLen");
+    return 1;
+}
+
+/* ---- verbose dumps, in EC/dump.c's format ---- */
+/* dumpCodingMatrix (EC/dump.c:46-59): n2 rows of n1 entries, decimal */
+static void dump_coding_matrix(const unsigned char* buf, int n1, int n2)
+{
+    for (int i = 0; i < n2; i++) {
+        for (int j = 0; j < n1; j++)
+            printf(" %d", buf[j + i * n1]);
+        printf("\n");
+    }
+    printf("\n");
+}
+
+/* dumpEncoder (EC/dump.c:61-73) */
+static void dump_encoder(const elect_ec_coder* c)
+{
+    unsigned char em[ELECT_EC_MAX_UNITS * ELECT_EC_MAX_DATA_UNITS] = {0};
+    int k = elect_ec_coder_num_data_units(c), m = elect_ec_coder_num_parity_units(c);
+    elect_ec_coder_encode_matrix(c, em, sizeof em);
+    printf("Encoding (numAllUnits = %d, numParityUnits = %d, numDataUnits = %d)\n", k + m, m, k);
+    printf("\n\nEncodeMatrix:\n");
+    dump_coding_matrix(em, k, k + m);
+    fflush(stdout);
+}
+
+/* dumpDecoder (EC/dump.c:75-104).  The reference's invert and decode matrices
+ * live in zeroed MMAX x KMAX arrays (clearDecoder, EC/erasure_coder.c:229-238),
+ * so rows past k (invert) and past numErased (decode) print as zeros. */
+static void dump_decoder(const elect_ec_coder* c, const int* dec, const int* era, int n_era, int mode)
+{
+    unsigned char em[ELECT_EC_MAX_UNITS * ELECT_EC_MAX_DATA_UNITS] = {0};
+    unsigned char inv[ELECT_EC_MAX_UNITS * ELECT_EC_MAX_DATA_UNITS] = {0};
+    unsigned char dm[ELECT_EC_MAX_UNITS * ELECT_EC_MAX_DATA_UNITS] = {0};
+    int k = elect_ec_coder_num_data_units(c), n = k + elect_ec_coder_num_parity_units(c);
+    if (elect_ec_coder_decode_matrix(c, dec, era, n_era, mode, dm) < 0 || elect_ec_coder_invert_matrix(c, dec, inv) < 0)
+        return;  /* an invalid call: the decode itself raises */
+    elect_ec_coder_encode_matrix(c, em, sizeof em);
+    printf("Recovering (numAllUnits = %d, numDataUnits = %d, numErased = %d)\n", n, k, n_era);
+    printf(" - ErasedIndexes = ");
+    for (int j = 0; j < n_era; j++)
+        printf(" %d", era[j]);
+    printf("       - DecodeIndex = ");
+    for (int i = 0; i < k; i++)
+        printf(" %d", dec[i]);
+    printf("\n\nEncodeMatrix:\n");
+    dump_coding_matrix(em, k, n);
+    printf("InvertMatrix:\n");
+    dump_coding_matrix(inv, k, n);
+    printf("DecodeMatrix:\n");
+    dump_coding_matrix(dm, k, n);
+    fflush(stdout);
 }
 
 /* setCoder, EC/jni_common.c:24-33 */
@@ -145,15 +229,16 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeImpl(JNIEnv* env,
 {
     unsigned char* in[2 + EC_MAX];
     unsigned char* out[2 + EC_MAX];
-    elect_ec_coder* c = get_coder(env, thiz);
-    if (c == NULL) {
-        throw_java(env, "java/io/IOException", "NativeRSRawEncoder closed");
+    elect_ec_coder* c = coder_for_call(env, thiz, "NativeRSRawEncoder closed");
+    int v;
+    if (c == NULL || (v = verbose(env, thiz)) < 0 || bad_length(env, dataLen))
         return;
-    }
     int k = elect_ec_coder_num_data_units(c), m = elect_ec_coder_num_parity_units(c);
     if (buffers(env, inputs, inputOffsets, k, in, "Invalid inputs") ||
         buffers(env, outputs, outputOffsets, m, out, "Invalid outputs"))
         return;
+    if (v)
+        dump_encoder(c);
     raise_status(env, elect_ec_encode(c, (const unsigned char* const*)in, out, (size_t)dataLen), "encode");
 }
 
@@ -167,15 +252,16 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeUpdateImpl(JNIEnv
 {
     unsigned char* in[2 + EC_MAX];
     unsigned char* out[2 + EC_MAX];
-    elect_ec_coder* c = get_coder(env, thiz);
-    if (c == NULL) {
-        throw_java(env, "java/io/IOException", "NativeRSRawEncoder closed");
+    elect_ec_coder* c = coder_for_call(env, thiz, "NativeRSRawEncoder closed");
+    int v;
+    if (c == NULL || (v = verbose(env, thiz)) < 0 || bad_length(env, dataLen))
         return;
-    }
     int m = elect_ec_coder_num_parity_units(c);
     if (buffers(env, inputs, inputOffsets, 2 + m, in, "Invalid inputs") ||
         buffers(env, outputs, outputOffsets, m, out, "Invalid outputs"))
         return;
+    if (v)
+        dump_encoder(c);
     raise_status(env,
                  elect_ec_encode_update(c, (const unsigned char* const*)in, targetUpdateDataIndex, out,
                                         (size_t)dataLen),
@@ -231,16 +317,17 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeExImpl(JNIEnv* en
     size_t lens[EC_MAX];
     const size_t* use_lens;
     jint h[EC_MAX];
-    elect_ec_coder* c = get_coder(env, thiz);
-    if (c == NULL) {
-        throw_java(env, "java/io/IOException", "NativeRSRawEncoder closed");
+    elect_ec_coder* c = coder_for_call(env, thiz, "NativeRSRawEncoder closed");
+    int v;
+    if (c == NULL || (v = verbose(env, thiz)) < 0 || bad_length(env, dataLen))
         return;
-    }
     int k = elect_ec_coder_num_data_units(c), m = elect_ec_coder_num_parity_units(c);
     if (buffers(env, inputs, inputOffsets, k, in, "Invalid inputs") ||
         buffers(env, outputs, outputOffsets, m, out, "Invalid outputs") ||
         content_lengths(env, contentLengths, k, lens, &use_lens) || hash_array(env, parityHashes, m))
         return;
+    if (v)
+        dump_encoder(c);
     if (raise_status(env,
                      elect_ec_encode_ex(c, (const unsigned char* const*)in, use_lens, out, (size_t)dataLen,
                                         parityHashes ? (int32_t*)h : NULL),
@@ -260,16 +347,17 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeUpdateExImpl(
     size_t lens[EC_MAX];
     const size_t* use_lens;
     jint h[EC_MAX];
-    elect_ec_coder* c = get_coder(env, thiz);
-    if (c == NULL) {
-        throw_java(env, "java/io/IOException", "NativeRSRawEncoder closed");
+    elect_ec_coder* c = coder_for_call(env, thiz, "NativeRSRawEncoder closed");
+    int v;
+    if (c == NULL || (v = verbose(env, thiz)) < 0 || bad_length(env, dataLen))
         return;
-    }
     int m = elect_ec_coder_num_parity_units(c);
     if (buffers(env, inputs, inputOffsets, 2 + m, in, "Invalid inputs") ||
         buffers(env, outputs, outputOffsets, m, out, "Invalid outputs") ||
         content_lengths(env, contentLengths, 2, lens, &use_lens) || hash_array(env, parityHashes, m))
         return;
+    if (v)
+        dump_encoder(c);
     if (raise_status(env,
                      elect_ec_encode_update_ex(c, (const unsigned char* const*)in, use_lens, targetUpdateDataIndex,
                                                out, (size_t)dataLen, parityHashes ? (int32_t*)h : NULL),
@@ -314,12 +402,14 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_decodeImpl(JNIEnv* env,
     unsigned char* in[2 + EC_MAX];
     unsigned char* out[2 + EC_MAX];
     int dec[EC_MAX], era[EC_MAX];
-    elect_ec_coder* c = get_coder(env, thiz);
-    if (c == NULL) {
-        throw_java(env, "java/io/IOException", "NativeRSRawDecoder closed");
+    elect_ec_coder* c = coder_for_call(env, thiz, "NativeRSRawDecoder closed");
+    int v;
+    if (c == NULL || (v = verbose(env, thiz)) < 0 || bad_length(env, dataLen))
         return;
-    }
-    int k = elect_ec_coder_num_data_units(c);
+    int k = elect_ec_coder_num_data_units(c), m = elect_ec_coder_num_parity_units(c);
+    if (v)  /* EC/NativeRSDecoder.c:57 */
+        printf("NativeRSDecoder_decodeImpl, start to process: data unit = %d, parity unit = %d, data block size = %d\n",
+               k, m, (int)dataLen);
     int n_dec = (*env)->GetArrayLength(env, decodeIndexes);
     int n_era = (*env)->GetArrayLength(env, erasedIndexes);
     if (n_dec < k || n_era > EC_MAX) {
@@ -328,12 +418,16 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_decodeImpl(JNIEnv* env,
     }
     (*env)->GetIntArrayRegion(env, decodeIndexes, 0, k, (jint*)dec);
     (*env)->GetIntArrayRegion(env, erasedIndexes, 0, n_era, (jint*)era);
-    if (verbose(env, thiz))
-        printf("NativeRSDecoder_decodeImpl: k=%d erased=%d first=%d len=%d\n", k, n_era,
-               n_era > 0 ? era[0] : -1, (int)dataLen);
+    if (v)  /* :65 */
+        printf("NativeRSDecoder_decodeImpl, read data: target recovery data block number = %d, the first recovery "
+               "request block ID = %d\n", n_era, n_era > 0 ? era[0] : 0);
     if (buffers(env, inputs, inputOffsets, k, in, "Invalid inputs") ||
         buffers(env, outputs, outputOffsets, n_era, out, "Invalid outputs"))
         return;
+    if (v) {  /* :68, then processErasures' dumpDecoder (EC/erasure_coder.c:195-197) */
+        printf("NativeRSDecoder_decodeImpl, start do decode\n");
+        dump_decoder(c, dec, era, n_era, decode_mode());
+    }
     raise_status(env,
                  elect_ec_decode(c, (const unsigned char* const*)in, dec, era, n_era, out, (size_t)dataLen,
                                  decode_mode()),
@@ -355,11 +449,10 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_decodeExImpl(JNIEnv* en
     int dec[EC_MAX], era[EC_MAX];
     size_t lens[EC_MAX];
     const size_t* use_lens;
-    elect_ec_coder* c = get_coder(env, thiz);
-    if (c == NULL) {
-        throw_java(env, "java/io/IOException", "NativeRSRawDecoder closed");
+    elect_ec_coder* c = coder_for_call(env, thiz, "NativeRSRawDecoder closed");
+    int v;
+    if (c == NULL || (v = verbose(env, thiz)) < 0 || bad_length(env, dataLen))
         return;
-    }
     int k = elect_ec_coder_num_data_units(c);
     int n_dec = (*env)->GetArrayLength(env, decodeIndexes);
     int n_era = (*env)->GetArrayLength(env, erasedIndexes);
@@ -373,6 +466,8 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_decodeExImpl(JNIEnv* en
         buffers(env, outputs, outputOffsets, n_era, out, "Invalid outputs") ||
         content_lengths(env, contentLengths, k, lens, &use_lens))
         return;
+    if (v)
+        dump_decoder(c, dec, era, n_era, decode_mode());
     raise_status(env,
                  elect_ec_decode_ex(c, (const unsigned char* const*)in, use_lens, dec, era, n_era, out,
                                     (size_t)dataLen, decode_mode()),

@@ -737,10 +737,18 @@ ScratchCache g_scratch[64];
 // Returns with entry->mu held; scratch_release() records the event and unlocks.
 hipError_t scratch_lease(hipStream_t stream, size_t words, ScratchEntry** out)
 {
+    // The scratch is allocated on, and cached for, the current device: a stream of
+    // another device would have its kernels read memory of the wrong device.
     int dev = 0;
     hipError_t err = hipGetDevice(&dev);
     if (err != hipSuccess) return err;
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (stream) {
+        hipDevice_t sdev = 0;
+        err = hipStreamGetDevice(stream, &sdev);
+        if (err != hipSuccess) return err;
+        if (sdev != dev) return hipErrorInvalidValue;  // include/elect_ec.h: streams of the current device
+    }
     ScratchCache& c = g_scratch[dev];
     for (;;) {
         ScratchEntry* e = nullptr;
@@ -1200,18 +1208,21 @@ hipError_t launch_apply_impl(const ApplyParams& p_in, hipStream_t stream)
     if (p_in.cols < 1 || p_in.cols > kMaxCols || p_in.rows < 1 || p_in.rows > kMaxRows) return hipErrorInvalidValue;
     if (p_in.stripes == 0) return hipSuccess;
     ApplyParams p = p_in;
-    if (p.hashes && p.cols > kMaxHashCols) return hipErrorInvalidValue;  // hashes are an encode feature
+    // Hashed launches wider than the widest hashed vector instance (an update of
+    // an m >= 9 code: 2 + m columns) take the byte-granular kernel, which adds
+    // its hash terms atomically (seeded below).
+    const bool wide_hash = p.hashes && p.cols > kMaxHashCols;
     p.aligned16 = apply_is_aligned(p);
     const bool vec = p.aligned16 || unaligned_vector_ok();  // dwordx4 kernels usable
     const uint32_t tiles = std::max<uint32_t>(1, p.tiles);
     const uint64_t ulen = p.unit_len ? p.unit_len : p.len;
     if (tiles > 1 && (!p.padded || p.len == 0 || p.len % 16 || p.stripes % tiles || ulen > tiles * p.len ||
-                      !vec || p.cols > kMaxPadCols))
+                      !vec || p.cols > kMaxPadCols || wide_hash))
         return hipErrorInvalidValue;  // tiling rides on the padded vector kernels only
     if (p.hashes && p.hash_seed) {
         // Assign mode needs the fast kernel with >= 64 segments per hashed unit
         // (every wave within two units); anything else seeds the entries and adds.
-        const bool fast = vec && (!p.padded || p.cols <= kMaxPadCols);
+        const bool fast = vec && (!p.padded || p.cols <= kMaxPadCols) && !wide_hash;
         const uint64_t segs = (p.padded ? (p.len + 15) / 16 : p.len / 16) * tiles;
         if (!fast || segs < 64) {
             const hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.hashes), static_cast<int>(pow31(ulen)),
@@ -1224,7 +1235,7 @@ hipError_t launch_apply_impl(const ApplyParams& p_in, hipStream_t stream)
     if (p.padded) {
         for (int j = 0; j < p.cols; ++j)
             if ((!p.lens || (p.lens_cols && j >= p.lens_cols)) && p.clen[j] > ulen) return hipErrorInvalidValue;
-        if (!vec || p.cols > kMaxPadCols) return launch_bytes(p, stream);
+        if (!vec || p.cols > kMaxPadCols || wide_hash) return launch_bytes(p, stream);
         for (int r0 = 0; r0 < p.rows; r0 += kFastRows) {
             const int nr = std::min(kFastRows, p.rows - r0);
             const hipError_t e = kFastPad[p.cols - 1][nr - 1](p, r0, stream);
@@ -1232,7 +1243,7 @@ hipError_t launch_apply_impl(const ApplyParams& p_in, hipStream_t stream)
         }
         return hipSuccess;
     }
-    if (!vec) return launch_bytes(p, stream);
+    if (!vec || wide_hash) return launch_bytes(p, stream);
     for (int r0 = 0; r0 < p.rows; r0 += kFastRows) {
         const int nr = std::min(kFastRows, p.rows - r0);
         const hipError_t e = kFast[p.cols - 1][nr - 1](p, r0, stream);

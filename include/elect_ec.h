@@ -128,6 +128,11 @@ int elect_ec_coder_gf_tables(const elect_ec_coder* coder, unsigned char* out, si
 int elect_ec_coder_decode_matrix(const elect_ec_coder* coder, const int* decode_indexes,
                                  const int* erased_indexes, int num_erased, int mode,
                                  unsigned char* out);
+/* k x k inverse of the survivor rows of the generator, in decode_indexes order
+ * (gf_invert_matrix, EC/erasure_coder.c:257-258).  A singular survivor set
+ * leaves the partially reduced matrix gf_invert_matrix stops at, with
+ * ELECT_EC_WARN_SINGULAR.  For the verbose dumps (EC/dump.c:76-104). */
+int elect_ec_coder_invert_matrix(const elect_ec_coder* coder, const int* decode_indexes, unsigned char* out);
 
 /* ---- host memory, synchronous: the JNI calling convention ----
  * Replace encode / encodeUpdate / decode (EC/erasure_coder.h:77-79, bodies at
@@ -178,7 +183,8 @@ int elect_ec_encode_ex(const elect_ec_coder* coder, const unsigned char* const* 
  * (old_new_lengths[0..1], NULL = both full; a NULL data pointer is allowed for a
  * zero length), P'[r] = P[r] ^ E[k+r][target] * (old ^ new) (ec_encode_data_update,
  * EC/erasure_coder.c:100-142), and hashCode() of every new parity unit (hashes,
- * NULL = not wanted; needs m <= 8).  Inputs [old, new, P0..Pm-1] as
+ * NULL = not wanted; codes with m >= 9 hash on the byte-granular kernel).
+ * Inputs [old, new, P0..Pm-1] as
  * elect_ec_encode_update; outputs may alias the old parity. */
 int elect_ec_encode_update_ex(const elect_ec_coder* coder, const unsigned char* const* old_new_parity,
                               const size_t* old_new_lengths, int target_data_index,
@@ -228,7 +234,8 @@ int elect_ec_encode_update_batch(const elect_ec_coder* coder, size_t chunk_size,
  * d_data_lengths: DEVICE uint32 [num_stripes][k] (NULL = all full);
  * d_old_new_lengths: DEVICE uint32 [num_stripes][2], old then new content
  * length (NULL = both full); d_hashes: DEVICE int32 [num_stripes][m], overwritten
- * (NULL = not wanted; the update needs m <= 8 for it).  parity_out may equal
+ * (NULL = not wanted; an update of an m >= 9 code hashes on the byte-granular
+ * kernel, and its tiled form needs m <= 8).  parity_out may equal
  * parity_in (in place). */
 int elect_ec_encode_batch_ex(const elect_ec_coder* coder, size_t chunk_size, size_t num_stripes,
                              elect_ec_shards data, const uint32_t* d_data_lengths, elect_ec_shards parity,

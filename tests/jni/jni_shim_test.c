@@ -21,6 +21,7 @@
 #include <dlfcn.h>
 #include <jni.h>
 #include <stdarg.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -35,6 +36,7 @@ struct _jobject {
     const char* cls;
     jlong native_coder;
     jboolean verbose;
+    int verbose_throws; /* allowVerboseDump() throws */
     unsigned char* addr;
     jobject* elems;
     jint* ints;
@@ -138,7 +140,17 @@ static jboolean m_CallBooleanMethod(JNIEnv* env, jobject o, jmethodID mid, ...)
 {
     (void)env;
     no_pending("CallBooleanMethod");
+    if (mid == (jmethodID)2 && o->verbose_throws) {
+        raise_exc("java/lang/IllegalStateException", "allowVerboseDump threw");
+        return JNI_FALSE;
+    }
     return mid == (jmethodID)2 ? o->verbose : JNI_FALSE;
+}
+
+static jboolean m_ExceptionCheck(JNIEnv* env)
+{
+    (void)env;  /* exception-safe per the JNI spec */
+    return vm.pending ? JNI_TRUE : JNI_FALSE;
 }
 
 static jlong m_GetLongField(JNIEnv* env, jobject o, jfieldID f)
@@ -230,12 +242,27 @@ static void m_DeleteLocalRef(JNIEnv* env, jobject o)
     if (o) --vm.local_refs;
 }
 
+/* The JNI specification's table layout (tests/jni/mock/jni.h pins every slot's
+ * index); the slots the shim does not call stay NULL, so calling one crashes. */
 static const struct JNINativeInterface_ kEnvTable = {
-    m_FindClass,         m_ThrowNew,           m_ExceptionClear,        m_GetObjectClass,
-    m_GetFieldID,        m_GetMethodID,        m_CallBooleanMethod,     m_GetLongField,
-    m_SetLongField,      m_GetArrayLength,     m_GetObjectArrayElement, m_GetIntArrayElements,
-    m_ReleaseIntArrayElements, m_GetIntArrayRegion, m_SetIntArrayRegion, m_GetDirectBufferAddress,
-    m_DeleteLocalRef,
+    .FindClass = m_FindClass,
+    .ThrowNew = m_ThrowNew,
+    .ExceptionClear = m_ExceptionClear,
+    .DeleteLocalRef = m_DeleteLocalRef,
+    .GetObjectClass = m_GetObjectClass,
+    .GetMethodID = m_GetMethodID,
+    .CallBooleanMethod = m_CallBooleanMethod,
+    .GetFieldID = m_GetFieldID,
+    .GetLongField = m_GetLongField,
+    .SetLongField = m_SetLongField,
+    .GetArrayLength = m_GetArrayLength,
+    .GetObjectArrayElement = m_GetObjectArrayElement,
+    .GetIntArrayElements = m_GetIntArrayElements,
+    .ReleaseIntArrayElements = m_ReleaseIntArrayElements,
+    .GetIntArrayRegion = m_GetIntArrayRegion,
+    .SetIntArrayRegion = m_SetIntArrayRegion,
+    .ExceptionCheck = m_ExceptionCheck,
+    .GetDirectBufferAddress = m_GetDirectBufferAddress,
 };
 static JNIEnv kEnv = &kEnvTable;
 static JNIEnv* env = &kEnv;
@@ -435,6 +462,20 @@ static int cpu_checks(void)
         EXPECT(threw("java/io/IOException", "no HIP device"));
     }
 
+    /* negative dataLen on the encoder's methods */
+    jni.encode(env, enc, in4, off4, -1, out2, poff2);
+    EXPECT(threw("java/lang/IllegalArgumentException", "negative dataLen"));
+    jni.update(env, enc, in4, off4, -16, 0, out2, poff2);
+    EXPECT(threw("java/lang/IllegalArgumentException", "negative dataLen"));
+    jni.encode_ex(env, enc, in4, off4, NULL, -2, out2, poff2, NULL);
+    EXPECT(threw("java/lang/IllegalArgumentException", "negative dataLen"));
+    jni.update_ex(env, enc, in4, off4, NULL, -3, 0, out2, poff2, NULL);
+    EXPECT(threw("java/lang/IllegalArgumentException", "negative dataLen"));
+    enc->verbose_throws = 1;
+    jni.encode(env, enc, in4, off4, 16, out2, poff2);
+    EXPECT(threw("java/lang/IllegalStateException", "allowVerboseDump"));
+    enc->verbose_throws = 0;
+
     /* destroy zeroes the field; use after destroy -> IOException (EC/NativeRSEncoder.c:46-50) */
     jni.enc_destroy(env, enc);
     EXPECT(clean());
@@ -472,10 +513,29 @@ static int cpu_checks(void)
     jni.decode_ex(env, dec, in4, off4, NULL, 16, int_array(3, di3), int_array(1, er1), out1, poff1);
     EXPECT(threw("java/lang/InternalError", "Invalid decode/erased indexes"));
 
-    /* an object without the nativeCoder field -> UnsatisfiedLinkError (EC/jni_common.h:29-36) */
+    /* an object without the nativeCoder field -> UnsatisfiedLinkError (EC/jni_common.h:29-36),
+     * on init and on every coding call (and nothing else thrown while it is pending) */
     jobject alien = coder_obj("java/lang/Object");
     jni.enc_init(env, alien, 4, 2);
     EXPECT(threw("java/lang/UnsatisfiedLinkError", "nativeCoder"));
+    jni.encode(env, alien, in4, off4, 16, out2, poff2);
+    EXPECT(threw("java/lang/UnsatisfiedLinkError", "nativeCoder"));
+    jni.decode(env, alien, in4, off4, 16, int_array(4, di4), int_array(1, er1), out1, poff1);
+    EXPECT(threw("java/lang/UnsatisfiedLinkError", "nativeCoder"));
+    jni.update_ex(env, alien, in4, off4, NULL, 16, 0, out2, poff2, NULL);
+    EXPECT(threw("java/lang/UnsatisfiedLinkError", "nativeCoder"));
+
+    /* a negative dataLen (a Java int) -> IllegalArgumentException, never a huge size_t */
+    jni.decode(env, dec, in4, off4, -5, int_array(4, di4), int_array(1, er1), out1, poff1);
+    EXPECT(threw("java/lang/IllegalArgumentException", "negative dataLen"));
+    jni.decode_ex(env, dec, in4, off4, NULL, -1, int_array(4, di4), int_array(1, er1), out1, poff1);
+    EXPECT(threw("java/lang/IllegalArgumentException", "negative dataLen"));
+
+    /* allowVerboseDump() throwing: its exception propagates, nothing else runs */
+    dec->verbose_throws = 1;
+    jni.decode(env, dec, in4, off4, 16, int_array(4, di4), int_array(1, er1), out1, poff1);
+    EXPECT(threw("java/lang/IllegalStateException", "allowVerboseDump"));
+    dec->verbose_throws = 0;
 
     jni.dec_destroy(env, dec);
     EXPECT(clean());
@@ -678,14 +738,63 @@ static int gpu_fused_flows(void)
     return failures;
 }
 
+/* ---- dump: allowVerboseDump() == true, the coder dumps on stdout ---------- *
+ * Prints "=== <case>" before each call; the calls' own results (the data, or
+ * an IOException without a device) are not part of the dump and are cleared. */
+static int dump_cases(void)
+{
+    struct Bufs d, p;
+    bufs_init(&d, 8, 16, 1);
+    bufs_init(&p, 4, 16, 2);
+    jobject enc = coder_obj(ENC_CLS), dec = coder_obj(DEC_CLS), dec12 = coder_obj(DEC_CLS);
+    enc->verbose = dec->verbose = dec12->verbose = JNI_TRUE;
+    jni.enc_init(env, enc, 4, 2);
+    jni.dec_init(env, dec, 4, 2);
+    jni.dec_init(env, dec12, 8, 4);
+    EXPECT(clean());
+    jobject in4 = obj_array(4, d.bb), off4 = int_array(4, d.pos);
+    jobject in8 = obj_array(8, d.bb), off8 = int_array(8, d.pos);
+    jobject out1 = obj_array(1, p.bb), poff1 = int_array(1, p.pos);
+    jobject out2 = obj_array(2, p.bb), poff2 = int_array(2, p.pos);
+    printf("=== encode RS(6,4)\n");
+    fflush(stdout);
+    jni.encode(env, enc, in4, off4, 16, out2, poff2);
+    vm.pending = 0;
+    const jint di[4] = {4, 1, 2, 3}, er[1] = {0}, ds[4] = {1, 1, 2, 3}, er2[2] = {0, 5};
+    printf("=== decode RS(6,4) {4,1,2,3} erase {0}\n");
+    fflush(stdout);
+    jni.decode(env, dec, in4, off4, 16, int_array(4, di), int_array(1, er), out1, poff1);
+    vm.pending = 0;
+    printf("=== decode RS(6,4) singular {1,1,2,3} erase {0,5}\n");
+    fflush(stdout);
+    jni.decode(env, dec, in4, off4, 16, int_array(4, ds), int_array(2, er2), out2, poff2);
+    vm.pending = 0;
+    const jint di12[8] = {2, 3, 4, 5, 6, 7, 8, 10}, er12[2] = {9, 0};
+    printf("=== decode RS(12,8) {2..8,10} erase {9,0}\n");
+    fflush(stdout);
+    jni.decode(env, dec12, in8, off8, 16, int_array(8, di12), int_array(2, er12), out2, poff2);
+    vm.pending = 0;
+    printf("=== end\n");
+    jni.enc_destroy(env, enc);
+    jni.dec_destroy(env, dec);
+    jni.dec_destroy(env, dec12);
+    EXPECT(vm.violations == 0);
+    return failures;
+}
+
 int main(int argc, char** argv)
 {
     if (argc < 3) {
-        fprintf(stderr, "usage: %s LIB cpu | LIB gpu OUTDIR\n", argv[0]);
+        fprintf(stderr, "usage: %s LIB cpu | LIB dump | LIB gpu OUTDIR\n", argv[0]);
         return 2;
     }
     load(argv[1]);
     const int gpu = !strcmp(argv[2], "gpu");
+    if (!strcmp(argv[2], "dump")) {
+        const int rc = dump_cases();
+        fprintf(stderr, "dump: %d failure(s), %d JNI violation(s)\n", rc, vm.violations);
+        return rc == 0 ? 0 : 1;
+    }
     int rc = gpu ? gpu_erasure_code_test(argc > 3 ? argv[3] : ".") : cpu_checks();
     if (gpu && rc == 0) rc = gpu_fused_flows();
     printf("%s: %d failure(s), %d JNI violation(s)\n", argv[2], rc, vm.violations);

@@ -649,3 +649,40 @@ print("fallback ok")
     env = dict(__import__("os").environ, ELECT_EC_BATCH_ARENA_MB=str(64 << 20))  # 64 TiB per arena
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0 and "fallback ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("k,m", [(3, 9), (2, 12), (5, 9)])
+def test_hashed_update_of_wide_codes(dev, oracle, k, m):
+    """encode_update_ex with hashes for m >= 9 (2 + m columns, wider than the
+    hashed vector kernels): the byte-granular kernel's atomic hash path, on the
+    device API and the host path; bit-exact parity and ByteBuffer.hashCode()."""
+    from elect_amd.batch import encode_update_batch_ex
+    from elect_amd.coder import RSCoder
+    rng = np.random.default_rng(k * 100 + m)
+    B, L, t = 3, 1000 + 7, k - 1
+    coder = RSCoder(k, m)
+    enc = oracle.Encoder(k, m)
+    old, new = _rand(rng, B, L), _rand(rng, B, L)
+    pin = _rand(rng, B, m, L)
+    lens = np.array([[L, L], [17, 900], [0, L]], np.int32)
+    pout = torch.zeros((B, m, L), dtype=torch.uint8, device=dev)
+    hashes = torch.zeros((B, m), dtype=torch.int32, device=dev)
+    encode_update_batch_ex(coder, t, _to(dev, old), _to(dev, new), _to(dev, pin), pout,
+                           lengths=_to(dev, lens), hashes=hashes)
+    got, gh = pout.cpu().numpy(), hashes.cpu().numpy()
+    for s in range(B):
+        o = np.where(np.arange(L) < lens[s, 0], old[s], 0).astype(np.uint8)
+        n = np.where(np.arange(L) < lens[s, 1], new[s], 0).astype(np.uint8)
+        want = enc.encode_update([o, n] + [pin[s, r] for r in range(m)], t)
+        for r in range(m):
+            assert np.array_equal(got[s, r], want[r]), (s, r)
+            assert int(gh[s, r]) == oracle.java_hashcode(want[r]), (s, r)
+    # host path (JNI encodeUpdateExImpl convention)
+    s = 1
+    outs = [np.zeros(L, np.uint8) for _ in range(m)]
+    ins = [old[s], new[s]] + [np.ascontiguousarray(pin[s, r]) for r in range(m)]
+    hs = coder.encode_update_ex_host([x.ctypes.data for x in ins], t, [x.ctypes.data for x in outs], L,
+                                     old_new_lengths=[int(lens[s, 0]), int(lens[s, 1])], hashed=True)
+    for r in range(m):
+        assert np.array_equal(outs[r], got[s, r])
+        assert hs[r] == int(gh[s, r])

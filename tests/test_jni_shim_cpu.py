@@ -6,7 +6,10 @@ Covers SURVEY.md §8b: the seven exported names (JEC/NativeRSEncoder.java:97-105
 JEC/NativeRSDecoder.java:81-87), the `long nativeCoder` ownership protocol
 (EC/jni_common.c:24-60), direct-buffer + offset resolution (EC/jni_common.c:62-108),
 and the exceptions Java callers see.  No device needed."""
+import re
 import subprocess
+
+import numpy as np
 
 from tests.jni_build import build
 
@@ -42,3 +45,68 @@ def test_shim_error_paths_under_fake_jvm():
     r = subprocess.run([drv, lib, "cpu"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failure(s), 0 JNI violation(s)" in r.stdout
+
+
+def _coding_matrix(buf, n1, n2):
+    """EC/dump.c:46-59 dumpCodingMatrix: n2 rows of n1 entries, ' %d' each."""
+    buf = list(buf) + [0] * (n1 * n2 - len(buf))
+    return "".join("".join(f" {buf[j + i * n1]}" for j in range(n1)) + "\n" for i in range(n2)) + "\n"
+
+
+def _decoder_block(oracle, k, m, dec, era, L):
+    n = k + m
+    em = oracle.cauchy_matrix(k, m).reshape(-1)
+    rows = np.stack([oracle.cauchy_matrix(k, m)[i] for i in dec])
+    _, inv = oracle.invert_matrix(rows)
+    _, dm = oracle.decode_matrix(k, m, dec, era, False)
+    return ("NativeRSDecoder_decodeImpl, start to process: data unit = %d, parity unit = %d, data block size = %d\n"
+            % (k, m, L) +
+            "NativeRSDecoder_decodeImpl, read data: target recovery data block number = %d, the first recovery "
+            "request block ID = %d\n" % (len(era), era[0]) +
+            "NativeRSDecoder_decodeImpl, start do decode\n" +
+            "Recovering (numAllUnits = %d, numDataUnits = %d, numErased = %d)\n" % (n, k, len(era)) +
+            " - ErasedIndexes = " + "".join(f" {e}" for e in era) +
+            "       - DecodeIndex = " + "".join(f" {d}" for d in dec) +
+            "\n\nEncodeMatrix:\n" + _coding_matrix(em, k, n) +
+            "InvertMatrix:\n" + _coding_matrix(inv.reshape(-1), k, n) +
+            "DecodeMatrix:\n" + _coding_matrix(dm.reshape(-1), k, n))
+
+
+def test_verbose_dumps_match_reference_format(oracle):
+    """allowVerboseDump() == true: the shim prints EC/dump.c's dumpEncoder
+    (:61-73) and dumpDecoder (:75-104) blocks, after decodeImpl's three lines
+    (EC/NativeRSDecoder.c:57, 65, 68), with the oracle's matrices: the Cauchy
+    generator, gf_invert_matrix's (partial, when singular) inverse in a zeroed
+    MMAX x KMAX array, and the compat decode rows."""
+    import re
+    lib, drv = build()
+    r = subprocess.run([drv, lib, "dump"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    cases = dict(re.findall(r"=== (.*?)\n(.*?)(?==== )", r.stdout, flags=re.S))
+    em = oracle.cauchy_matrix(4, 2).reshape(-1)
+    assert cases["encode RS(6,4)"] == ("Encoding (numAllUnits = 6, numParityUnits = 2, numDataUnits = 4)\n"
+                                       "\n\nEncodeMatrix:\n" + _coding_matrix(em, 4, 6))
+    assert cases["decode RS(6,4) {4,1,2,3} erase {0}"] == _decoder_block(oracle, 4, 2, [4, 1, 2, 3], [0], 16)
+    assert cases["decode RS(6,4) singular {1,1,2,3} erase {0,5}"] == \
+        _decoder_block(oracle, 4, 2, [1, 1, 2, 3], [0, 5], 16)
+    assert cases["decode RS(12,8) {2..8,10} erase {9,0}"] == \
+        _decoder_block(oracle, 8, 4, [2, 3, 4, 5, 6, 7, 8, 10], [9, 0], 16)
+
+
+def test_mock_jni_table_is_the_specification_layout():
+    """The mock header the shim is built against pins every slot it uses to the
+    JNI specification's function-table index (compile-time asserts), so the
+    tested library calls the same slots a JDK-built one does."""
+    import os
+    from tests.conftest import ROOT
+    text = open(os.path.join(ROOT, "tests", "jni", "mock", "jni.h")).read()
+    want = {"FindClass": 6, "ThrowNew": 14, "ExceptionClear": 17, "DeleteLocalRef": 23, "GetObjectClass": 31,
+            "GetMethodID": 33, "CallBooleanMethod": 37, "GetFieldID": 94, "GetLongField": 101, "SetLongField": 110,
+            "GetArrayLength": 171, "GetObjectArrayElement": 173, "GetIntArrayElements": 187,
+            "ReleaseIntArrayElements": 195, "GetIntArrayRegion": 203, "SetIntArrayRegion": 211,
+            "ExceptionCheck": 228, "GetDirectBufferAddress": 230}
+    for name, idx in want.items():
+        assert f"JNI_SLOT({name}, {idx});" in text, name
+    shim = open(os.path.join(ROOT, "elect_amd", "csrc", "jni", "libec_jni.c")).read()
+    used = set(re.findall(r"\(\*env\)->(\w+)", shim))
+    assert used <= set(want), used - set(want)

@@ -81,6 +81,10 @@ for step in "$@"; do
     gputests)  # a subset: GPU_TESTS="tests/test_gpu_tiled.py ..."
         run pytest_gpu_subset 900 python -m pytest ${GPU_TESTS} -m gpu -x -q -p no:cacheprovider --timeout 300
         rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
+    hosttile)  # batcher arena tiled (64 KiB) vs untiled, ELECT's codeLength, interleaved 3x
+        for i in 1 2 3; do for tk in 64 0; do for T in ${BATCH_THREADS:-64 16}; do
+            ELECT_EC_BATCH_TILE_KB=$tk run "bench_hostpath_tile${tk}_T${T}_$i" 300 python bench.py --config hostpath --threads $T --host-op ${HOST_OP:-encode} || exit $?
+        done; done; done ;;
     hostsweep) run hostsweep 600 python tools/tune/host_sweep.py || exit $? ;;
     copysizes) run copysizes 600 python tools/tune/host_sweep.py copysizes || exit $? ;;
     staged)
