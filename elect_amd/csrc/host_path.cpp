@@ -3,6 +3,8 @@
 // (EC/NativeRSEncoder.c:43-61 -> EC/erasure_coder.c:74-98).
 #include "host_path.hpp"
 
+#include <emmintrin.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -21,6 +23,41 @@ namespace host {
 namespace {
 
 using kern::ApplyParams;
+
+// Host copies into and out of the pinned staging memory, with non-temporal
+// (streaming) stores: the data is not read again by this CPU (the DMA engine
+// reads the arena; the caller reads its output later), so write-allocate reads
+// of the destination lines would only double the host-DRAM traffic this path
+// is bound by.  glibc's memcpy streams only above its non-temporal threshold,
+// which 64 KiB tile copies are far below.  Callers fence (_mm_sfence) before
+// the data is handed on.
+void stream_copy(uint8_t* dst, const uint8_t* src, size_t n)
+{
+#ifndef AB_NO_STREAM_COPY
+    if (n >= 4096) {
+        const size_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
+        std::memcpy(dst, src, head);
+        dst += head;
+        src += head;
+        n -= head;
+        const size_t body = n & ~size_t{63};
+        for (size_t i = 0; i < body; i += 64) {
+            const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+            const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+            const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+            const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+        }
+        dst += body;
+        src += body;
+        n -= body;
+    }
+#endif
+    std::memcpy(dst, src, n);
+}
 
 // ---------------------------------------------------------------------------
 // Host-memory path: per-thread, per-device staging engine.
@@ -69,7 +106,8 @@ public:
                 if (e != hipSuccess) return map_hip(e);
                 const size_t o = pending[s] * step;
                 const size_t n = std::min(step, len - o);
-                for (int r = 0; r < op.rows; ++r) std::memcpy(op.out[r] + o, pin_out_[s] + r * pitch, n);
+                for (int r = 0; r < op.rows; ++r) stream_copy(op.out[r] + o, pin_out_[s] + r * pitch, n);
+                _mm_sfence();
                 busy[s] = false;
             }
             if (c >= nchunks) continue;
@@ -82,12 +120,14 @@ public:
                     const size_t v = op.lens[j] > o ? std::min(n, op.lens[j] - o) : 0;
                     valid[j] = static_cast<uint32_t>(v);
                     if (v == 0) continue;
-                    std::memcpy(pin_in_[s] + j * pitch, op.in[j] + o, v);
+                    stream_copy(pin_in_[s] + j * pitch, op.in[j] + o, v);
+                    _mm_sfence();
                     e = hipMemcpyAsync(d_in_[s] + j * pitch, pin_in_[s] + j * pitch, v, hipMemcpyHostToDevice,
                                        stream_[s]);
                 }
             } else {
-                for (int j = 0; j < op.cols; ++j) std::memcpy(pin_in_[s] + j * pitch, op.in[j] + o, n);
+                for (int j = 0; j < op.cols; ++j) stream_copy(pin_in_[s] + j * pitch, op.in[j] + o, n);
+                _mm_sfence();
                 e = hipMemcpyAsync(d_in_[s], pin_in_[s], op.cols * pitch, hipMemcpyHostToDevice, stream_[s]);
             }
             if (e == hipSuccess) e = launch(op, s, pitch, n, op.lens ? valid : nullptr, o);
@@ -324,6 +364,7 @@ public:
         if (!started_) {  // arenas, streams and events once, before anything is in flight
             if (init(batch_config().arena_bytes.load()) != ELECT_EC_OK) {
                 release();  // whatever the failed attempt got; callers use the per-thread engine
+                (void)hipGetLastError();
                 init_failed_ = true;
                 return kFallback;
             }
@@ -363,8 +404,9 @@ public:
             const size_t n = op.lens ? op.lens[j] : len;  // padded: only the content bytes
             if (op.lens) slab->pin_lens[static_cast<size_t>(slot) * op.cols + j] = static_cast<uint32_t>(n);
             for (size_t o = 0; o < n; o += pitch)  // untiled: pitch >= len, one copy
-                std::memcpy(in_base + (o / pitch * op.cols + j) * pitch, op.in[j] + o, std::min(pitch, n - o));
+                stream_copy(in_base + (o / pitch * op.cols + j) * pitch, op.in[j] + o, std::min(pitch, n - o));
         }
+        _mm_sfence();  // the streamed stores are visible before the dispatcher's H2D reads them
 
         lock.lock();
         if (++slab->filled == slab->reserved) cv_worker_.notify_one();
@@ -378,8 +420,9 @@ public:
             for (int r = 0; r < op.rows; ++r)
                 for (size_t t = 0; t < tiles; ++t) {
                     const size_t o = t * pitch;
-                    std::memcpy(op.out[r] + o, out_base + (t * op.rows + r) * pitch, tiles > 1 ? std::min(pitch, len - o) : len);
+                    stream_copy(op.out[r] + o, out_base + (t * op.rows + r) * pitch, tiles > 1 ? std::min(pitch, len - o) : len);
                 }
+            _mm_sfence();
             if (op.hashes)
                 std::memcpy(op.hashes, slab->pin_hash + static_cast<size_t>(slot) * op.rows, op.rows * sizeof(int32_t));
         }

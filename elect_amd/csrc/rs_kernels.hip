@@ -1205,6 +1205,10 @@ bool apply_is_aligned(const ApplyParams& p)
 
 hipError_t launch_apply_impl(const ApplyParams& p_in, hipStream_t stream)
 {
+    // Launch errors are read back with hipGetLastError, which also returns an
+    // earlier failure of any HIP call on this thread (a failed hipMalloc, say):
+    // drop that first, so only this call's launches are judged.
+    (void)hipGetLastError();
     if (p_in.cols < 1 || p_in.cols > kMaxCols || p_in.rows < 1 || p_in.rows > kMaxRows) return hipErrorInvalidValue;
     if (p_in.stripes == 0) return hipSuccess;
     ApplyParams p = p_in;
@@ -1272,6 +1276,7 @@ hipError_t launch_apply(const ApplyParams& p_in, hipStream_t stream)
 
 hipError_t launch_update(const UpdateParams& p, hipStream_t stream)
 {
+    (void)hipGetLastError();  // as launch_apply_impl
     if (p.rows < 1 || p.rows > kMaxRows || p.rows + 2 > kMaxCols) return hipErrorInvalidValue;
     if (p.len == 0 || p.stripes == 0) return hipSuccess;
     bool aligned = col_aligned(p.old_data) && col_aligned(p.new_data);

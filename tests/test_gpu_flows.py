@@ -105,18 +105,29 @@ def test_encode_update_batch_ex(dev, oracle, k, m, L, padded, hashed, in_place):
                 assert int(got_h[s, r]) == oracle.java_hashcode(want[r]), (s, r)
 
 
-def test_update_ex_hash_needs_m_le_8(dev):
+def test_tiled_update_hash_needs_m_le_8(dev):
+    """A hashed update of an m >= 9 code runs on the byte-granular kernel
+    (tests/test_gpu_parity.py::test_hashed_update_of_wide_codes), which has no
+    tiled form: the tiled call refuses it; untiled and unhashed tiled calls run."""
     from elect_amd import _lib
-    from elect_amd.batch import encode_update_batch_ex
+    from elect_amd.batch import encode_update_batch_ex, encode_update_batch_tiled
     from elect_amd.coder import RSCoder
     B, L, m = 2, 64, 9
     z = torch.zeros((B, L), dtype=torch.uint8, device=dev)
     p = torch.zeros((B, m, L), dtype=torch.uint8, device=dev)
+    h = torch.zeros((B, m), dtype=torch.int32, device=dev)
     with pytest.raises(_lib.ECInvalidArgument):
-        encode_update_batch_ex(RSCoder(4, m), 0, z, z, p, p, hashes=torch.zeros((B, m), dtype=torch.int32,
-                                                                                  device=dev))
-    encode_update_batch_ex(RSCoder(4, m), 0, z, z, p, p, lengths=torch.zeros((B, 2), dtype=torch.int32,
-                                                                             device=dev))  # padded alone is fine
+        encode_update_batch_tiled(RSCoder(4, m), 0, z, z, p, p, L, hashes=h)
+    encode_update_batch_tiled(RSCoder(4, m), 0, z, z, p, p, L)
+    encode_update_batch_ex(RSCoder(4, m), 0, z, z, p, p, hashes=h)
+    torch.cuda.synchronize()
+    assert not p.any()  # all-zero units: zero parity, hash 31^L
+    assert all(int(x) == _pow31(L) for x in h.view(-1).cpu())
+
+
+def _pow31(n):
+    v = pow(31, n, 1 << 32)
+    return v - (1 << 32) if v >= 1 << 31 else v
 
 
 def test_elect_flow_encode_then_update(dev, oracle):

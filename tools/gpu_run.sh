@@ -81,10 +81,12 @@ for step in "$@"; do
     gputests)  # a subset: GPU_TESTS="tests/test_gpu_tiled.py ..."
         run pytest_gpu_subset 900 python -m pytest ${GPU_TESTS} -m gpu -x -q -p no:cacheprovider --timeout 300
         rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
-    hosttile)  # batcher arena tiled (64 KiB) vs untiled, ELECT's codeLength, interleaved 3x
-        for i in 1 2 3; do for tk in 64 0; do for T in ${BATCH_THREADS:-64 16}; do
-            ELECT_EC_BATCH_TILE_KB=$tk run "bench_hostpath_tile${tk}_T${T}_$i" 300 python bench.py --config hostpath --threads $T --host-op ${HOST_OP:-encode} || exit $?
-        done; done; done ;;
+    hosttile)  # batcher arena tiled (64 KiB) vs untiled, ELECT's codeLength, interleaved 3x;
+               # AB_VARIANTS=b also runs elect_amd/_ab/libelect_ec_b.so (e.g. built with -DAB_NO_STREAM_COPY)
+        for i in 1 2 3; do for v in a ${AB_VARIANTS:-}; do for tk in 64 0; do for T in ${BATCH_THREADS:-64 16}; do
+            lib=""; [ $v = a ] || lib="$PWD/elect_amd/_ab/libelect_ec_$v.so"
+            ELECT_EC_LIB=$lib ELECT_EC_BATCH_TILE_KB=$tk run "bench_hostpath_${v}_tile${tk}_T${T}_$i" 300 python bench.py --config hostpath --threads $T --host-op ${HOST_OP:-encode} || exit $?
+        done; done; done; done ;;
     hostsweep) run hostsweep 600 python tools/tune/host_sweep.py || exit $? ;;
     copysizes) run copysizes 600 python tools/tune/host_sweep.py copysizes || exit $? ;;
     staged)
