@@ -707,6 +707,37 @@ inline int block_for(uint64_t len, int coefs) { return (len <= 4096 || coefs >= 
 
 constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches are encodes
 
+// Occupancy cap for the plain streaming kernel (gf_apply_x16 without padding
+// or hash): dynamic LDS that no block reads, so that at most `waves` waves of a
+// launch are resident per CU (160 KiB of LDS per CU / blocks).  Fewer waves in
+// flight keep fewer HBM pages open at once.  Measured (occupancy
+// sweep, 3 interleaved rounds): uncapped (32 waves) -> 20 waves: RS(6,4) decode
+// 77.3 -> 81.0 % of peak, the mixed config +3 %, RS(12,8) decode 77 -> 80 %;
+// encodes (R >= K/2: more writes in flight) peak at 24.  The padded, hashed and
+// update kernels lost with any cap (their length loads and epilogues want the
+// waves: ELECT's fused steps 80 -> 67 % at 20) and run uncapped.
+#ifndef AB_WAVES_READ_HEAVY
+#define AB_WAVES_READ_HEAVY 20
+#endif
+#ifndef AB_WAVES_WRITE_HEAVY
+#define AB_WAVES_WRITE_HEAVY 24
+#endif
+constexpr size_t kLdsPerCU = 160 * 1024;
+
+inline int plain_waves_cap(int cols, int rows)
+{
+    return 2 * rows >= cols ? AB_WAVES_WRITE_HEAVY : AB_WAVES_READ_HEAVY;
+}
+
+inline size_t cap_lds(int block, int coefs, int waves)
+{
+    if (waves <= 0) return 0;
+    const int blocks = std::max(1, waves / (block / 64));
+    const size_t static_lds = static_cast<size_t>(coefs) * kTabStride * sizeof(uint32_t);
+    const size_t per_block = kLdsPerCU / blocks - 512;  // > kLdsPerCU / (blocks + 1): one block fewer fits
+    return per_block > static_lds ? per_block - static_lds : 0;
+}
+
 // Hash-partial scratch when the caller brings none (the device-resident API):
 // one buffer per (device, stream), reused only in that stream's order, grown or
 // handed to another stream only after an event recorded behind its last use.
@@ -876,7 +907,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         if (!lens_path) {
             const uint32_t grid = (a.total + block - 1) / block;
             if (!a.hashes) {
-                hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, false>), dim3(grid), dim3(block), 0, stream, a);
+                hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, false>), dim3(grid), dim3(block),
+                                   PAD ? 0 : cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
             } else if constexpr (K <= kMaxHashCols) {
                 hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, true>), dim3(grid), dim3(block), 0, stream, a);
             }  // (launch_apply rejects hashed launches wider than kMaxHashCols)
