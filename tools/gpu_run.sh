@@ -34,6 +34,15 @@ for step in "$@"; do
             -- python3 bench.py --no-cpu --no-host --no-sizes --steps 5 --warmup 1 || exit $?
         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run \
             -- python3 bench.py --no-cpu --no-host --no-sizes --steps 5 --warmup 1 || exit $? ;;
+    pmcab)  # decode vs encode, occupancy-capped (a) vs uncapped (u): HBM request queue depth and stalls
+        PA="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_LEVEL_sum GRBM_GUI_ACTIVE"
+        PB="TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum TCC_TOO_MANY_EA_WRREQS_STALL_sum GRBM_GUI_ACTIVE"
+        for v in a u; do for pass in A B; do
+            lib=""; [ $v = a ] || lib="$PWD/elect_amd/_ab/libelect_ec_$v.so"
+            ctr=$PA; [ $pass = B ] && ctr=$PB
+            ELECT_EC_LIB=$lib run pmcab_${v}_$pass 120 rocprofv3 --pmc $ctr --output-format csv -d $OUT/pmcab_${v}_$pass -o run \
+                -- python3 bench.py --no-cpu --no-host --no-sizes --steps 5 --warmup 1 || exit $?
+        done; done ;;
     profcfg)  # rocprof kernel stats of one bench config: PROF_CFG="--config hashed ..."
         run profcfg 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profcfg_$TAG -o run \
             -- python3 bench.py ${PROF_CFG:-} --no-cpu --no-host --steps 20 --warmup 3 || exit $? ;;
