@@ -713,8 +713,9 @@ constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches ar
 // flight keep fewer HBM pages open at once.  Measured (occupancy
 // sweep, 3 interleaved rounds): uncapped (32 waves) -> 20 waves: RS(6,4) decode
 // 77.3 -> 81.0 % of peak, the mixed config +3 %, RS(12,8) decode 77 -> 80 %;
-// encodes (R >= K/2: more writes in flight) peak at 24.  The padded, hashed and
-// update kernels lost with any cap (their length loads and epilogues want the
+// encodes (R >= K/2: more writes in flight) peak at 24.  PMC: the uncapped
+// decode waits on DRAM read credits 6x as often (profiles/r02_pmc_occupancy_ab.txt).
+// The hashed and update kernels lost with any cap (the hash epilogue wants the
 // waves: ELECT's fused steps 80 -> 67 % at 20) and run uncapped.
 #ifndef AB_WAVES_READ_HEAVY
 #define AB_WAVES_READ_HEAVY 20
@@ -727,6 +728,18 @@ constexpr size_t kLdsPerCU = 160 * 1024;
 inline int plain_waves_cap(int cols, int rows)
 {
     return 2 * rows >= cols ? AB_WAVES_WRITE_HEAVY : AB_WAVES_READ_HEAVY;
+}
+
+inline size_t cap_lds(int block, int coefs, int waves);
+
+// The padded per-stripe-length kernel takes the same cap: 64 KiB degraded-read
+// decode (flows) 76.4 -> 77.4 %, padded encodes unchanged (3 interleaved rounds).
+#ifndef AB_CAP_LENS
+#define AB_CAP_LENS 1
+#endif
+inline size_t lens_cap(int block, int coefs, int cols, int rows)
+{
+    return AB_CAP_LENS ? cap_lds(block, coefs, AB_CAP_LENS > 1 ? AB_CAP_LENS : plain_waves_cap(cols, rows)) : 0;
 }
 
 inline size_t cap_lds(int block, int coefs, int waves)
@@ -901,7 +914,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                 constexpr int U = lens_unroll<K>();
                 const uint64_t threads = (static_cast<uint64_t>(a.total) + 64 * U - 1) / (64 * U) * 64;
                 hipLaunchKernelGGL((gf_apply_lens<K, R, U>), dim3(static_cast<uint32_t>((threads + block - 1) / block)),
-                                   dim3(block), 0, stream, a);
+                                   dim3(block), lens_cap(block, R * K, K, R), stream, a);
             }
         }
         if (!lens_path) {
