@@ -71,6 +71,10 @@ for step in "$@"; do
         run bench_rehearse_2rank 600 python bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu || exit $?
         run bench_rehearse_2rank_mixed 600 python bench.py --gpus 2 --config mixed --steps 10 || exit $?
         unset ELECT_BENCH_SHARE_GPU ;;
+    multirank8)  # the 8-rank plumbing on the one GPU (gloo; every rank's kernels share the device)
+        export ELECT_BENCH_SHARE_GPU=1
+        run bench_rehearse_8rank 600 python bench.py --gpus 8 --steps 10 --warmup 2 --no-cpu --no-host --rotate 2 || exit $?
+        unset ELECT_BENCH_SHARE_GPU ;;
     graph)  # host submit time: eager vs HIP-graph replay, headline and mixed
         run bench_eager_nosizes 300 python bench.py --no-cpu --no-host --no-sizes --steps 50 || exit $?
         run bench_graph 300 python bench.py --graph --no-cpu --no-host --no-sizes --steps 50 || exit $?
@@ -110,6 +114,8 @@ for step in "$@"; do
         run bench_mixed 400 python bench.py --config mixed || exit $?
         run bench_rs12 400 python bench.py --config rs12 || exit $?
         run bench_hostpath 400 python bench.py --config hostpath || exit $?
+        run bench_hostpath_T64 400 python bench.py --config hostpath --threads 64 || exit $?
+        run bench_hostpath_T64_encode_ex 400 python bench.py --config hostpath --threads 64 --host-op encode_ex || exit $?
         run bench_update 400 python bench.py --config update || exit $?
         run bench_padded 400 python bench.py --config padded || exit $?
         run bench_hashed 400 python bench.py --config hashed || exit $?
