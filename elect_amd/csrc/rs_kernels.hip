@@ -923,6 +923,9 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                 hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, false>), dim3(grid), dim3(block),
                                    PAD ? 0 : cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
             } else if constexpr (K <= kMaxHashCols) {
+                // (uncapped: capping the hashed instance at 24 / 28 waves per CU cost it 5 / 3
+                // points, and staging 31^(16*lane) in LDS instead of constant memory gained
+                // nothing; profiles/r02_hash_ab/)
                 hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, true>), dim3(grid), dim3(block), 0, stream, a);
             }  // (launch_apply rejects hashed launches wider than kMaxHashCols)
         }
