@@ -92,6 +92,13 @@ def parse():
                          "0: untiled)")
     ap.add_argument("--flows-inplace", action="store_true",
                     help="flows: the update writes the new parity over the old (ELECT writes separate buffers)")
+    ap.add_argument("--mixed-group", type=int, default=1, choices=(0, 1),
+                    help="mixed: code the size classes through elect_ec_{encode,decode}_batches (one launch "
+                         "for all classes each, the default) or one call per class (0)")
+    ap.add_argument("--mixed-streams", type=int, default=1,
+                    help="mixed: issue the size classes on this many streams (1: one stream, in order)")
+    ap.add_argument("--mixed-share", type=int, default=0,
+                    help="mixed: code rank 0's share of an N-rank partition on this GPU (strong-scaling probe)")
     ap.add_argument("--graph", action="store_true",
                     help="headline and mixed: capture each step's launches in a HIP graph and replay it")
     ap.add_argument("--launch-check", action="store_true",
@@ -448,21 +455,53 @@ def config_mixed(args, world, rank, dev):
     """BASELINE configs[3]: RS(6,4) encode + decode (erase 0) over three size
     classes, 1 GiB of data per class in total, each class byte-balanced over
     the ranks (strong scaling: total work fixed)."""
-    from elect_amd.batch import decode_batch, encode_batch, partition_by_bytes
+    from elect_amd.batch import decode_batch, decode_batches, encode_batch, encode_batches, partition_by_bytes
     from elect_amd.coder import RSCoder
     k, m = 4, 2
     coder = RSCoder(k, m)
     classes = []
+    # --mixed-share N: code only rank 0's share of an N-rank partition on this one GPU (what
+    # each GPU of an N-GPU run does under strong scaling), to see the per-GPU rate there
+    parts, prank = (args.mixed_share, 0) if args.mixed_share else (world, rank)
+    share_bytes = 0
     for L in (1024, 4096, 1 << 20):
         total = (1 << 30) // (k * L)
-        b, e = partition_by_bytes([k * L] * total, world, rank)
+        b, e = partition_by_bytes([k * L] * total, parts, prank)
+        share_bytes += 2 * (e - b) * k * L
         st, Bc, Lc = alloc_stripes(args, e - b, L, k, m, dev)
         classes.append((L, st, torch.empty((Bc, 1, Lc), dtype=torch.uint8, device=dev)))
 
+    # --mixed-streams S: the classes are independent batches; with S > 1 class i is issued on
+    # stream i % S behind an event from the step's stream (and joined back at the end), so
+    # one class's launch tail overlaps the next class's ramp-up
+    main = torch.cuda.current_stream()
+    streams = [main] if args.mixed_streams <= 1 else [torch.cuda.Stream() for _ in range(args.mixed_streams)]
+
+    enc_pairs = [(st[:, :k], st[:, k:]) for _, st, _ in classes]
+    dec_pairs = [(st, out) for _, st, out in classes]
+
+    def step_grouped():  # elect_ec_encode_batches / _decode_batches: one launch for all classes each
+        encode_batches(coder, enc_pairs)
+        decode_batches(coder, dec_pairs, [1, 2, 3, 4], [0], inputs_by_unit=True)
+
     def step():
-        for L, st, out in classes:
-            encode_batch(coder, st[:, :k], st[:, k:])
-            decode_batch(coder, st, [1, 2, 3, 4], [0], out, inputs_by_unit=True)
+        if args.mixed_group:
+            return step_grouped()
+        cur = torch.cuda.current_stream()
+        if len(streams) > 1:
+            start = torch.cuda.Event()
+            start.record(cur)
+        for i, (L, st, out) in enumerate(classes):
+            s_i = cur if len(streams) == 1 else streams[i % len(streams)]
+            if s_i is not cur:
+                s_i.wait_event(start)
+            with torch.cuda.stream(s_i):
+                encode_batch(coder, st[:, :k], st[:, k:])
+                decode_batch(coder, st, [1, 2, 3, 4], [0], out, inputs_by_unit=True)
+            if s_i is not cur:
+                done = torch.cuda.Event()
+                done.record(s_i)
+                cur.wait_event(done)
 
     run = graph_steps([step])[0] if args.graph else step
     dt, submit = timed(run, args.steps, args.warmup, world)
@@ -485,11 +524,20 @@ def config_mixed(args, world, rank, dev):
         enc_ms, dec_ms = sorted(t["encode"])[4], sorted(t["decode"])[4]
         per_class[f"{L}B"] = {"encode_frac": round(B * (k + m) * Lc / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                               "decode_frac": round(B * (k + 1) * Lc / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    if args.mixed_share:  # one GPU's share of an N-GPU run, timed alone: its own rate, and N x it
+        per_gpu = args.steps * share_bytes / dt / GIB
+        return {"metric": f"GiB/s device-resident RS(6,4) encode+decode, mixed chunks: one GPU's share of an "
+                          f"{parts}-GPU strong-scaled run", "value": round(per_gpu, 2), "unit": "GiB/s (this GPU)",
+                "n_gpus": world, "share_of": parts, "aggregate_if_ranks_scale": round(parts * per_gpu, 2),
+                "steps": args.steps, "ms_per_step": round(dt / args.steps * 1e3, 4),
+                "host_submit_ms_per_step": round(submit, 4), "graph": bool(args.graph),
+                "streams": len(streams), "grouped": bool(args.mixed_group), "verified": ok, "classes": per_class, "data": "synthetic", "dtype": "u8", "higher_is_better": True,
+                "config": {"workload": f"rank 0's byte-balanced share of 1 GiB per class split {parts} ways"}}
     return {"metric": "GiB/s device-resident RS(6,4) encode+decode, mixed 1 KiB/4 KiB/1 MiB chunks",
             "value": round(args.steps * data / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
-            "host_submit_ms_per_step": round(submit, 4), "graph": bool(args.graph),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+            "host_submit_ms_per_step": round(submit, 4), "graph": bool(args.graph), "streams": len(streams),
+            "grouped": bool(args.mixed_group), "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic", "verified": ok, "classes": per_class,
             "config": {"layout": {f"{L}B": LAYOUT_NAMES[layout_for(args, L)] for L, _, _ in classes},
                        "workload": "RS(6,4) encode+decode (erase 0), 1 GiB data per class "

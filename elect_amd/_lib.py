@@ -57,6 +57,10 @@ class ColumnT(ctypes.Structure):
     _fields_ = [("ptr", ctypes.c_void_p), ("stripe_stride", ctypes.c_size_t)]
 
 
+class BatchT(ctypes.Structure):
+    _fields_ = [("chunk_size", ctypes.c_size_t), ("num_stripes", ctypes.c_size_t), ("inp", Shards), ("out", Shards)]
+
+
 _u8p = ctypes.POINTER(ctypes.c_ubyte)
 _u8pp = ctypes.POINTER(ctypes.c_void_p)
 _ip = ctypes.POINTER(ctypes.c_int)
@@ -116,6 +120,9 @@ SIGNATURES = [
     ("elect_ec_decode_batch_tiled", ctypes.c_int, [_cp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, Shards,
                                                    _cp, _ip, _ip, ctypes.c_int, Shards, ctypes.c_uint, ctypes.c_int,
                                                    _cp]),
+    ("elect_ec_encode_batches", ctypes.c_int, [_cp, ctypes.POINTER(BatchT), ctypes.c_int, _cp]),
+    ("elect_ec_decode_batches", ctypes.c_int, [_cp, ctypes.POINTER(BatchT), ctypes.c_int, _ip, _ip, ctypes.c_int,
+                                               ctypes.c_uint, ctypes.c_int, _cp]),
     ("elect_ec_apply_batch", ctypes.c_int, [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
                                             ctypes.c_size_t, ctypes.POINTER(ColumnT),
                                             ctypes.POINTER(ColumnT), _cp]),

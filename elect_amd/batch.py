@@ -205,6 +205,33 @@ def decode_batch_tiled(coder: RSCoder, inputs: torch.Tensor, decode_indexes, era
                  "decode_batch_tiled")
 
 
+def encode_batches(coder: RSCoder, pairs, stream=None) -> None:
+    """encode_batch over several (data [B_i, k, L_i], parity [B_i, m, L_i]) pairs of different
+    chunk sizes in as few launches as possible (elect_ec_encode_batches)."""
+    arr = (_lib.BatchT * max(1, len(pairs)))()
+    for i, (data, parity) in enumerate(pairs):
+        B, k, L = data.shape
+        if k != coder.k or parity.shape != (B, coder.m, L):
+            raise ValueError(f"shape mismatch: data {tuple(data.shape)} parity {tuple(parity.shape)}")
+        arr[i] = _lib.BatchT(L, B, _shards(data), _shards(parity))
+    check(lib.elect_ec_encode_batches(coder.handle, arr, len(pairs), _stream(stream)), "encode_batches")
+
+
+def decode_batches(coder: RSCoder, pairs, decode_indexes, erased, mode: int = _lib.DECODE_COMPAT,
+                   inputs_by_unit: bool = False, outputs_by_unit: bool = False, stream=None) -> int:
+    """decode_batch over several (inputs, outputs) pairs with one erasure pattern (elect_ec_decode_batches)."""
+    if len(decode_indexes) != coder.k:
+        raise ValueError("decode_indexes needs exactly k entries")
+    arr = (_lib.BatchT * max(1, len(pairs)))()
+    for i, (inputs, outputs) in enumerate(pairs):
+        B, _, L = inputs.shape
+        arr[i] = _lib.BatchT(L, B, _shards(inputs), _shards(outputs))
+    flags = (_lib.INPUTS_BY_UNIT if inputs_by_unit else 0) | (_lib.OUTPUTS_BY_UNIT if outputs_by_unit else 0)
+    return check(lib.elect_ec_decode_batches(coder.handle, arr, len(pairs), int_array(decode_indexes),
+                                             int_array(erased), len(erased), flags, mode, _stream(stream)),
+                 "decode_batches")
+
+
 def apply_batch(coef: np.ndarray, src, dst, stream=None) -> None:
     """dst[r] = XOR_j coef[r, j] * src[j] over [B, L] column tensors."""
     coef = np.ascontiguousarray(coef, np.uint8)

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "gf256.hpp"
 #include "host_path.hpp"
@@ -570,6 +571,60 @@ int elect_ec_encode_update_batch_tiled(const elect_ec_coder* coder, size_t chunk
     if (tile_bytes == 0) return ELECT_EC_EINVAL;
     return update_batch_impl(coder, chunk_size, tile_bytes, num_stripes, target_data_index, old_data, new_data,
                              d_old_new_lengths, parity_in, parity_out, d_hashes, stream);
+}
+
+int elect_ec_encode_batches(const elect_ec_coder* coder, const elect_ec_batch* batches, int num_batches,
+                            void* stream)
+{
+    if (!valid_coder(coder) || num_batches < 0 || (num_batches > 0 && !batches)) return ELECT_EC_EINVAL;
+    std::vector<ApplyParams> ps(static_cast<size_t>(num_batches));
+    for (int i = 0; i < num_batches; ++i) {
+        const elect_ec_batch& b = batches[i];
+        if (b.chunk_size && b.num_stripes && (!b.in.base || !b.out.base)) return ELECT_EC_EINVAL;
+        ApplyParams& p = ps[i];
+        p.len = b.chunk_size;
+        p.stripes = b.num_stripes;
+        p.cols = coder->k;
+        p.rows = coder->m;
+        for (int j = 0; j < p.cols; ++j) p.src[j] = col(b.in.base, b.in.stripe_stride, j * b.in.shard_stride);
+        for (int r = 0; r < p.rows; ++r) {
+            p.dst[r] = col(b.out.base, b.out.stripe_stride, r * b.out.shard_stride);
+            std::memcpy(p.coef + r * p.cols, parity_row(coder, r), coder->k);
+        }
+    }
+    return map_hip(elect::kern::launch_apply_many(ps.data(), num_batches, as_stream(stream)));
+}
+
+int elect_ec_decode_batches(const elect_ec_coder* coder, const elect_ec_batch* batches, int num_batches,
+                            const int* decode_indexes, const int* erased_indexes, int num_erased,
+                            unsigned flags, int mode, void* stream)
+{
+    if (!valid_coder(coder) || num_batches < 0 || (num_batches > 0 && !batches)) return ELECT_EC_EINVAL;
+    uint8_t coef[elect::kern::kMaxRows * elect::kern::kMaxCols] = {};
+    const int st = build_decode_matrix(coder, decode_indexes, erased_indexes, num_erased, mode, coef);
+    if (st < 0) return st;
+    if (num_erased == 0) return st;
+    std::vector<ApplyParams> ps(static_cast<size_t>(num_batches));
+    for (int i = 0; i < num_batches; ++i) {
+        const elect_ec_batch& b = batches[i];
+        if (b.chunk_size && b.num_stripes && (!b.in.base || !b.out.base)) return ELECT_EC_EINVAL;
+        ApplyParams& p = ps[i];
+        p.len = b.chunk_size;
+        p.stripes = b.num_stripes;
+        p.cols = coder->k;
+        p.rows = num_erased;
+        std::memcpy(p.coef, coef, sizeof(coef));
+        for (int j = 0; j < p.cols; ++j) {
+            const size_t slot = (flags & ELECT_EC_INPUTS_BY_UNIT) ? static_cast<size_t>(decode_indexes[j]) : j;
+            p.src[j] = col(b.in.base, b.in.stripe_stride, slot * b.in.shard_stride);
+        }
+        for (int r = 0; r < p.rows; ++r) {
+            const size_t slot = (flags & ELECT_EC_OUTPUTS_BY_UNIT) ? static_cast<size_t>(erased_indexes[r]) : r;
+            p.dst[r] = col(b.out.base, b.out.stripe_stride, slot * b.out.shard_stride);
+        }
+    }
+    const int rc = map_hip(elect::kern::launch_apply_many(ps.data(), num_batches, as_stream(stream)));
+    return rc != ELECT_EC_OK ? rc : st;
 }
 
 int elect_ec_apply_batch(const unsigned char* coef, int rows, int cols, size_t chunk_size, size_t num_stripes,

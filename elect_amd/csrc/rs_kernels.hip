@@ -32,6 +32,7 @@
 #include <array>
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "rs_kernels.hpp"
 
@@ -410,10 +411,10 @@ __device__ __forceinline__ void gf_combine(const uint4 (&x)[K], const uint32_t* 
 
 // Stage the byte-shuffle tables of a launch into LDS (8 dwords per coefficient).
 template <int K, int R>
-__device__ __forceinline__ void stage_tables(const FastArgs<K, R>& a, uint32_t* tl)
+__device__ __forceinline__ void stage_tables(const gf::PermTable (&tab)[R][K], uint32_t* tl)
 {
     for (int i = threadIdx.x; i < R * K; i += blockDim.x) {
-        const gf::PermTable& t = a.tab[i / K][i % K];
+        const gf::PermTable& t = tab[i / K][i % K];
         tl[i * kTabStride + 0] = t.t0_lo;
         tl[i * kTabStride + 1] = t.t0_hi;
         tl[i * kTabStride + 2] = t.t1_lo;
@@ -454,7 +455,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         tile_lengths<K>(a, s0, sl, true);
     }
 
-    stage_tables(a, tl);
+    stage_tables<K, R>(a.tab, tl);
     if (HASH ? first >= a.total : !live) return;  // HASH: only wholly dead waves leave
     if (!PAD) {
 #pragma unroll
@@ -580,7 +581,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
         uniform = s0 == stripe_of(min(first + 64u * U - 1u, a.total - 1u));
         tile_lengths<K>(a, s0, sl, true);
     }
-    stage_tables(a, tl);
+    stage_tables<K, R>(a.tab, tl);
     if (first >= a.total) return;
 
     if (uniform) {
@@ -652,6 +653,55 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
 #pragma unroll
         for (int r = 0; r < R; ++r) store_nt(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Grouped launch: several batches with the same coefficients (different chunk
+// sizes, strides and stripe counts) in ONE launch of the plain kernel body.
+// Block b belongs to the last part whose first block is <= b (a wave-uniform
+// scan over at most kMaxGroup parts).  A batch of small launches (a strong-
+// scaled mixed-size step at 8 GPUs: tens of microseconds each) otherwise pays
+// one ramp-up and one drain per batch.
+// ---------------------------------------------------------------------------
+constexpr int kMaxGroup = 8;
+
+template <int K, int R>
+struct GroupPart {
+    const uint8_t* sp[K];
+    uint64_t ss[K];
+    uint8_t* dp[R];
+    uint64_t ds[R];
+    uint32_t segs, total, magic, shift;
+    uint32_t block0;  // first block of this part
+};
+
+template <int K, int R>
+struct GroupArgs {
+    GroupPart<K, R> part[kMaxGroup];
+    int n;
+    gf::PermTable tab[R][K];
+};
+
+template <int K, int R>
+__global__ __launch_bounds__(kBlock) void gf_apply_group(const GroupArgs<K, R> a)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
+    int p = 0;
+    for (int q = 1; q < a.n; ++q)
+        if (blockIdx.x >= a.part[q].block0) p = q;
+    const GroupPart<K, R>& g = a.part[p];
+    const uint32_t idx = (blockIdx.x - g.block0) * blockDim.x + threadIdx.x;
+    stage_tables<K, R>(a.tab, tl);
+    if (idx >= g.total) return;
+    const uint32_t stripe = static_cast<uint32_t>((static_cast<uint64_t>(idx) * g.magic) >> g.shift);
+    const uint64_t off = static_cast<uint64_t>(idx - stripe * g.segs) * 16;
+    uint4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = load_nt(g.sp[j] + stripe * g.ss[j] + off);
+    uint4 acc[R];
+    gf_combine<K, R>(x, tl, acc);
+#pragma unroll
+    for (int r = 0; r < R; ++r) store_nt(g.dp[r] + stripe * g.ds[r] + off, acc[r]);
 }
 
 #ifndef AB_PAD_U4
@@ -964,6 +1014,59 @@ const std::array<std::array<FastFn, kFastRows>, kMaxPadCols> kFastPad = {
     fast_row_fns<1, true>(), fast_row_fns<2, true>(), fast_row_fns<3, true>(), fast_row_fns<4, true>(),
     fast_row_fns<5, true>(), fast_row_fns<6, true>(), fast_row_fns<7, true>(), fast_row_fns<8, true>(),
     fast_row_fns<9, true>(), fast_row_fns<10, true>()};
+
+// Launch parts [0, n) of a group (all plain, vector-capable, whole segments,
+// same coefficients) for output rows r0 .. r0+R-1.
+template <int K, int R>
+hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t stream)
+{
+    GroupArgs<K, R> a{};
+    a.n = n;
+    for (int r = 0; r < R; ++r)
+        for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(ps[0].coef[(r0 + r) * ps[0].cols + j]);
+    uint64_t len_max = 0;
+    for (int i = 0; i < n; ++i) len_max = std::max<uint64_t>(len_max, ps[i].len);
+    const int block = block_for(len_max, R * K);
+    uint64_t blocks = 0;
+    for (int i = 0; i < n; ++i) {
+        const ApplyParams& p = ps[i];
+        GroupPart<K, R>& g = a.part[i];
+        const uint64_t segs = p.len / 16;
+        g.segs = static_cast<uint32_t>(segs);
+        g.total = static_cast<uint32_t>(segs * p.stripes);
+        const Magic mg = make_magic(g.segs);
+        g.magic = mg.m;
+        g.shift = mg.p;
+        for (int j = 0; j < K; ++j) {
+            g.sp[j] = p.src[j].ptr;
+            g.ss[j] = p.src[j].stride;
+        }
+        for (int r = 0; r < R; ++r) {
+            g.dp[r] = const_cast<uint8_t*>(p.dst[r0 + r].ptr);
+            g.ds[r] = p.dst[r0 + r].stride;
+        }
+        g.block0 = static_cast<uint32_t>(blocks);
+        blocks += (g.total + block - 1) / block;
+    }
+    if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((gf_apply_group<K, R>), dim3(static_cast<uint32_t>(blocks)), dim3(block),
+                       cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
+    return hipGetLastError();
+}
+
+using GroupFn = hipError_t (*)(const ApplyParams*, int, int, hipStream_t);
+
+template <int K>
+constexpr std::array<GroupFn, kFastRows> group_row_fns()
+{
+    return {&launch_group_kr<K, 1>, &launch_group_kr<K, 2>, &launch_group_kr<K, 3>, &launch_group_kr<K, 4>};
+}
+
+const std::array<std::array<GroupFn, kFastRows>, kMaxCols> kGroup = {
+    group_row_fns<1>(),  group_row_fns<2>(),  group_row_fns<3>(),  group_row_fns<4>(),
+    group_row_fns<5>(),  group_row_fns<6>(),  group_row_fns<7>(),  group_row_fns<8>(),
+    group_row_fns<9>(),  group_row_fns<10>(), group_row_fns<11>(), group_row_fns<12>(),
+    group_row_fns<13>(), group_row_fns<14>(), group_row_fns<15>(), group_row_fns<16>()};
 
 // ---------------------------------------------------------------------------
 // Byte-granular path: any alignment, any (cols, rows) up to 16 x 16.
@@ -1320,6 +1423,58 @@ hipError_t launch_apply(const ApplyParams& p_in, hipStream_t stream)
     err = launch_apply_impl(p, stream);
     const hipError_t r = scratch_release(e, stream);
     return err != hipSuccess ? err : r;
+}
+
+// Several plain batches with one coefficient matrix: grouped into as few launches
+// as the group kernel allows (kMaxGroup parts, each under 2^31 segments, whole
+// 16-byte segments, vector kernels usable); anything else launches alone.
+hipError_t launch_apply_many(const ApplyParams* ps, int n, hipStream_t stream)
+{
+    (void)hipGetLastError();  // as launch_apply_impl
+    if (n < 0 || (n > 0 && !ps)) return hipErrorInvalidValue;
+    std::vector<ApplyParams> grouped;
+    for (int i = 0; i < n; ++i) {
+        ApplyParams p = ps[i];
+        if (p.cols < 1 || p.cols > kMaxCols || p.rows < 1 || p.rows > kMaxRows) return hipErrorInvalidValue;
+        if (i > 0 && (p.cols != ps[0].cols || p.rows != ps[0].rows ||
+                      std::memcmp(p.coef, ps[0].coef, sizeof(p.coef)) != 0))
+            return hipErrorInvalidValue;  // one coefficient matrix per call
+        if (p.stripes == 0 || p.len == 0) continue;
+        p.aligned16 = apply_is_aligned(p);
+        const bool groupable = !p.padded && !p.hashes && p.tiles <= 1 && p.len % 16 == 0 &&
+                               (p.len / 16) * p.stripes <= kMaxIndex && (p.aligned16 || unaligned_vector_ok());
+        if (groupable) {
+            grouped.push_back(p);
+            continue;
+        }
+        const hipError_t e = launch_apply_impl(p, stream);
+        if (e != hipSuccess) return e;
+    }
+    // Batches group with others of the same block-size class (block_for: small chunks
+    // run 128-thread blocks), in submission order within a class.
+    std::stable_sort(grouped.begin(), grouped.end(), [](const ApplyParams& x, const ApplyParams& y) {
+        return block_for(x.len, x.rows * x.cols) < block_for(y.len, y.rows * y.cols);
+    });
+    for (size_t g0 = 0; g0 < grouped.size();) {
+        const int cls = block_for(grouped[g0].len, grouped[g0].rows * grouped[g0].cols);
+        size_t g1 = g0 + 1;
+        while (g1 < grouped.size() && g1 - g0 < kMaxGroup && block_for(grouped[g1].len, grouped[g1].rows * grouped[g1].cols) == cls)
+            ++g1;
+        const int m = static_cast<int>(g1 - g0);
+        if (m == 1) {  // nothing to group with: the plain launcher
+            const hipError_t e = launch_apply_impl(grouped[g0], stream);
+            if (e != hipSuccess) return e;
+        } else {
+            const ApplyParams& p0 = grouped[g0];
+            for (int r0 = 0; r0 < p0.rows; r0 += kFastRows) {
+                const int nr = std::min(kFastRows, p0.rows - r0);
+                const hipError_t e = kGroup[p0.cols - 1][nr - 1](grouped.data() + g0, m, r0, stream);
+                if (e != hipSuccess) return e;
+            }
+        }
+        g0 = g1;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_update(const UpdateParams& p, hipStream_t stream)

@@ -111,6 +111,10 @@ struct UpdateParams {
 
 hipError_t launch_apply(const ApplyParams& p, hipStream_t stream);
 
+// n batches with the same cols, rows and coefficients: the plain ones (no padding,
+// hashes or tiles, whole segments) share grouped launches; the rest launch alone.
+hipError_t launch_apply_many(const ApplyParams* ps, int n, hipStream_t stream);
+
 // Scratch words a hashed launch_apply over `segments` 16-byte segments in all
 // (stripes x ceil(len/16)) needs at most (row groups run one after another).
 constexpr size_t hash_scratch_need(uint64_t segments) { return (segments / 64 + 1) * kFastRows * 2; }

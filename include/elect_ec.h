@@ -276,6 +276,24 @@ int elect_ec_decode_batch_tiled(const elect_ec_coder* coder, size_t chunk_size, 
                                 size_t num_stripes, elect_ec_shards inputs, const uint32_t* d_input_lengths,
                                 const int* decode_indexes, const int* erased_indexes, int num_erased,
                                 elect_ec_shards outputs, unsigned flags, int mode, void* stream);
+/* ---- several device batches in one call ----
+ * Batches of different chunk sizes (ELECT's mixed SSTable sizes, the mixed 1 KiB /
+ * 4 KiB / 1 MiB config) coded with one coder: the same bytes as one
+ * elect_ec_encode_batch / elect_ec_decode_batch per element, but batches with
+ * whole 16-byte segments share one launch (up to 8 per launch), so a step of
+ * many short batches pays one kernel ramp-up and drain instead of one per batch. */
+typedef struct elect_ec_batch {
+    size_t chunk_size;
+    size_t num_stripes;
+    elect_ec_shards in;   /* encode: data units; decode: survivors (or stripes, ELECT_EC_INPUTS_BY_UNIT) */
+    elect_ec_shards out;  /* encode: parity units; decode: rebuilt units (or stripes, ELECT_EC_OUTPUTS_BY_UNIT) */
+} elect_ec_batch;
+int elect_ec_encode_batches(const elect_ec_coder* coder, const elect_ec_batch* batches, int num_batches,
+                            void* stream);
+/* One erasure pattern for every batch. */
+int elect_ec_decode_batches(const elect_ec_coder* coder, const elect_ec_batch* batches, int num_batches,
+                            const int* decode_indexes, const int* erased_indexes, int num_erased,
+                            unsigned flags, int mode, void* stream);
 /* General product dst[r] = XOR_j coef[r*cols+j] * src[j], rows, cols <= 16. */
 int elect_ec_apply_batch(const unsigned char* coef, int rows, int cols, size_t chunk_size,
                          size_t num_stripes, const elect_ec_column* src,

@@ -686,3 +686,48 @@ def test_hashed_update_of_wide_codes(dev, oracle, k, m):
     for r in range(m):
         assert np.array_equal(outs[r], got[s, r])
         assert hs[r] == int(gh[s, r])
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (3, 5)])
+def test_encode_decode_batches_equal_per_batch_calls(dev, oracle, k, m):
+    """elect_ec_encode_batches / _decode_batches (several chunk sizes, one call):
+    the same bytes as one encode_batch / decode_batch per element.  Mixes
+    groupable batches (whole segments; more than 8 of them: two launches) with
+    ones that launch alone (L % 16 != 0, a misaligned base) and empty ones;
+    m = 5: two row groups; sampled stripes against the oracle."""
+    from elect_amd.batch import decode_batch, decode_batches, encode_batch, encode_batches
+    from elect_amd.coder import RSCoder
+    rng = np.random.default_rng(31 * k + m)
+    coder = RSCoder(k, m)
+    shapes = [(64, 1024), (9, 4096), (3, 65536), (5, 4099), (2, 48), (0, 1024), (7, 16), (4, 2048), (3, 1024),
+              (2, 8192), (6, 512), (1, 65536 + 16), (5, 160)]
+    stripes = []
+    for i, (B, L) in enumerate(shapes):
+        if i == 4:  # a misaligned base: the vector kernels still run it, alone
+            big = torch.zeros(B * (k + m) * L + 16, dtype=torch.uint8, device=dev)
+            st = big[3:3 + B * (k + m) * L].view(B, k + m, L)
+        else:
+            st = torch.zeros((B, k + m, L), dtype=torch.uint8, device=dev)
+        st[:, :k] = _to(dev, _rand(rng, B, k, L))
+        stripes.append(st)
+    encode_batches(coder, [(st[:, :k], st[:, k:]) for st in stripes])
+    ref = [torch.zeros_like(st[:, k:]) for st in stripes]
+    for st, r in zip(stripes, ref):
+        if st.shape[0]:
+            encode_batch(coder, st[:, :k], r)
+    torch.cuda.synchronize()
+    enc = oracle.Encoder(k, m)
+    for st, r in zip(stripes, ref):
+        assert torch.equal(st[:, k:], r)
+        if st.shape[0]:
+            h = st[-1].cpu().numpy()
+            want = enc.encode([h[j] for j in range(k)])
+            assert all(np.array_equal(h[k + q], want[q]) for q in range(m))
+    erased = [0, k] if m >= 2 else [0]
+    surv = [i for i in range(k + m) if i not in erased][:k]
+    outs = [torch.full((st.shape[0], len(erased), st.shape[2]), 0x5A, dtype=torch.uint8, device=dev) for st in stripes]
+    decode_batches(coder, list(zip(stripes, outs)), surv, erased, mode=1, inputs_by_unit=True)
+    torch.cuda.synchronize()
+    for st, o in zip(stripes, outs):
+        for q, e in enumerate(erased):
+            assert torch.equal(o[:, q], st[:, e])

@@ -80,6 +80,13 @@ for step in "$@"; do
         run bench_graph 300 python bench.py --graph --no-cpu --no-host --no-sizes --steps 50 || exit $?
         run bench_mixed_eager 300 python bench.py --config mixed --steps 20 || exit $?
         run bench_mixed_graph 300 python bench.py --config mixed --graph --steps 20 || exit $? ;;
+    mixedshare)  # the mixed config's per-GPU share at 2/4/8 GPUs, eager and graph-replayed
+        IFS=';' read -ra OPTS <<< "${SHARE_OPTS:-;--graph}"
+        [ ${#OPTS[@]} -eq 0 ] && OPTS=("")
+        for n in ${SHARES:-1 2 4 8}; do for g in "${OPTS[@]}"; do
+            tag=${g//[- ]/}
+            run "bench_mixed_share${n}_${tag:-eager}" 300 python bench.py --config mixed --mixed-share $n $g --steps 50 || exit $?
+        done; done ;;
     hostinfo)
         { echo "affinity=$(python -c 'import os;print(len(os.sched_getaffinity(0)))') nproc=$(nproc)";
           cat /sys/fs/cgroup/cpu.max /sys/fs/cgroup/pids.max 2>&1; lscpu | grep -E "Model name|^CPU\(s\)|NUMA node"; } \
