@@ -138,3 +138,109 @@ def test_fuzz_case(dev, oracle, i):
             assert (st == _lib.WARN_SINGULAR) == (rc == -1)
             for r in range(ne):
                 assert np.array_equal(got[s, r], want_d[r]), (i, "decode", mode, s, r, surv, erased)
+
+
+TILED_CASES = 24
+
+
+@pytest.mark.parametrize("i", range(TILED_CASES))
+def test_fuzz_tiled_case(dev, oracle, i):
+    """Seeded random tiled-unit cases (elect_ec_*_batch_tiled): a random tile size
+    (a multiple of 16, around and far below the unit), content lengths incl. 0,
+    full, above L and at tile edges, with and without hashes; encode, parity
+    update (new parity to a separate buffer) and a random-erasure decode, all
+    against the oracle on the zero-filled whole units."""
+    from elect_amd import _lib
+    from elect_amd.batch import decode_batch_tiled, encode_batch_tiled, encode_update_batch_tiled
+    from elect_amd.coder import RSCoder
+    rng = np.random.default_rng(0x711E + i)
+    k = int(rng.integers(1, 11))
+    m = int(rng.integers(1, min(8, 14 - k) + 1))
+    L = int(rng.choice([1, 17, 1000, 4099, 65536, 65540, 100003, 4404020 // 32 + 3]))
+    tile = int(rng.choice([16, 48, 1024, 4096, 65536, 16 * int(rng.integers(1, 300))]))
+    T = max(1, -(-L // tile))
+    B = int(rng.integers(1, 5))
+    hashed = bool(rng.integers(0, 2))
+    c = RSCoder(k, m)
+    enc = oracle.Encoder(k, m)
+
+    def tiled(units):  # [B, n, L] -> [B*T, n, tile] device view, pad 0xEE
+        n = units.shape[1]
+        pad = np.full((B, n, T * tile), 0xEE, np.uint8)
+        pad[:, :, :L] = units
+        blk = np.ascontiguousarray(pad.reshape(B, n, T, tile).transpose(0, 2, 1, 3))
+        return torch.from_numpy(blk).to(dev).view(B * T, n, tile)
+
+    def untiled(view):
+        n = view.shape[1]
+        return view.cpu().numpy().reshape(B, T, n, tile).transpose(0, 2, 1, 3).reshape(B, n, T * tile)[:, :, :L]
+
+    data = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    lens = _lengths(rng, B, k, L)
+    edges = [min(L, tile * int(rng.integers(0, T + 1)) + int(rng.choice([0, 1, -1]))) for _ in range(k)]
+    lens[0] = np.maximum(edges, 0)
+    eff = _clip(lens, L)
+    full = np.zeros_like(data)
+    shown = np.full_like(data, 0xAB)
+    for s in range(B):
+        for j in range(k):
+            full[s, j, :eff[s, j]] = data[s, j, :eff[s, j]]
+            shown[s, j, :eff[s, j]] = data[s, j, :eff[s, j]]
+    view = tiled(np.concatenate([shown, np.full((B, m, L), 0x5A, np.uint8)], axis=1))
+    hs = torch.zeros((B, m), dtype=torch.int32, device=dev) if hashed else None
+    encode_batch_tiled(c, view[:, :k], view[:, k:], L, lengths=torch.from_numpy(lens).to(dev), hashes=hs)
+    par = untiled(view[:, k:])
+    want = [enc.encode([full[s, j] for j in range(k)]) for s in range(B)]
+    for s in range(B):
+        for r in range(m):
+            assert np.array_equal(par[s, r], want[s][r]), (i, "encode", s, r)
+            if hashed:
+                assert int(hs[s, r]) == oracle.java_hashcode(want[s][r]), (i, "hash", s, r)
+
+    t = int(rng.integers(0, k))
+    new = rng.integers(0, 256, (B, L), dtype=np.uint8)
+    ul = _lengths(rng, B, 2, L)
+    ul[:, 0] = lens[:, t]
+    new_eff = _clip(ul[:, 1:2], L)[:, 0]
+    new_shown = np.full_like(new, 0xCD)
+    for s in range(B):
+        new_shown[s, :new_eff[s]] = new[s, :new_eff[s]]
+    new_view = tiled(new_shown[:, None])[:, 0]
+    pout = torch.full((B * T, m, tile), 0x33, dtype=torch.uint8, device=dev)
+    hu = torch.zeros((B, m), dtype=torch.int32, device=dev) if hashed else None
+    encode_update_batch_tiled(c, t, view[:, t], new_view, view[:, k:], pout, L,
+                              lengths=torch.from_numpy(np.ascontiguousarray(ul)).to(dev), hashes=hu)
+    full2 = full.copy()
+    for s in range(B):
+        full2[s, t] = 0
+        full2[s, t, :new_eff[s]] = new[s, :new_eff[s]]
+    got = untiled(pout)
+    want2 = [enc.encode([full2[s, j] for j in range(k)]) for s in range(B)]
+    for s in range(B):
+        for r in range(m):
+            assert np.array_equal(got[s, r], want2[s][r]), (i, "update", s, r)
+            if hashed:
+                assert int(hu[s, r]) == oracle.java_hashcode(want2[s][r]), (i, "update hash", s, r)
+
+    units = np.concatenate([full, np.stack([np.stack(w) for w in want])], axis=1)
+    ne = int(rng.integers(1, m + 1))
+    erased = [int(x) for x in rng.permutation(k + m)[:ne]]
+    surv = [int(u) for u in rng.permutation(k + m) if u not in erased][:k]
+    dlen = np.zeros((B, k), np.int32)
+    shown_units = np.full_like(units, 0xEE)
+    for s in range(B):
+        for jj, u in enumerate(surv):
+            n = int(np.max(np.nonzero(units[s, u])[0], initial=-1)) + 1 + int(rng.integers(0, 3))
+            dlen[s, jj] = min(L, n)
+            shown_units[s, u, :dlen[s, jj]] = units[s, u, :dlen[s, jj]]
+    iview = tiled(shown_units)
+    for mode in (_lib.DECODE_COMPAT, _lib.DECODE_STRICT):
+        out = torch.full((B * T, ne, tile), 0x11, dtype=torch.uint8, device=dev)
+        st = decode_batch_tiled(c, iview, surv, erased, out, L, lengths=torch.from_numpy(dlen).to(dev), mode=mode,
+                                inputs_by_unit=True)
+        got = untiled(out)
+        for s in range(B):
+            rc, want_d = oracle.decode(k, m, [units[s, u] for u in surv], surv, erased, strict=bool(mode))
+            assert (st == _lib.WARN_SINGULAR) == (rc == -1)
+            for r in range(ne):
+                assert np.array_equal(got[s, r], want_d[r]), (i, "decode", mode, s, r, surv, erased)
