@@ -324,6 +324,10 @@ struct BatchConfig {
     std::atomic<unsigned> window_us{0};
     std::atomic<size_t> arena_bytes{size_t{256} << 20};
     std::atomic<size_t> tile{size_t{1} << 16};  // ELECT_EC_BATCH_TILE_KB (0: untiled arena)
+    // ELECT_EC_BATCH_SLABS: arenas per device, 2..4.  Three let one batch fill while
+    // two are in flight (H2D + kernel, D2H + callers copying out): 64 callers on
+    // 4.4 MB stripes 37-44.5 -> 46-50 GiB/s against two (profiles/r02_hostslabs.txt).
+    std::atomic<int> slabs{3};
 };
 
 BatchConfig& batch_config()
@@ -334,6 +338,8 @@ BatchConfig& batch_config()
         const char* w = std::getenv("ELECT_EC_BATCH_WINDOW_US");
         const char* a = std::getenv("ELECT_EC_BATCH_ARENA_MB");
         const char* t = std::getenv("ELECT_EC_BATCH_TILE_KB");
+        const char* n = std::getenv("ELECT_EC_BATCH_SLABS");
+        if (n) c.slabs = std::min(4, std::max(2, std::atoi(n)));
         if (w) c.window_us = static_cast<unsigned>(std::atoi(w));
         if (a && std::atoll(a) > 0) c.arena_bytes = static_cast<size_t>(std::atoll(a)) << 20;
         if (t && std::atoi(t) >= 0) c.tile = static_cast<size_t>(std::atoi(t)) << 10;
@@ -346,7 +352,7 @@ BatchConfig& batch_config()
 class Batcher {
 public:
     static constexpr int kFallback = 1000;  // request does not fit (or no arena): run it directly
-    static constexpr int kSlabs = 2;
+    static constexpr int kMaxSlabs = 4;  // arenas per device (ELECT_EC_BATCH_SLABS, default 3)
     // Per-slot content lengths (padded ops) and parity hashes (hashed ops) of a
     // batch: entries per arena, which caps such a batch's stripes.
     static constexpr size_t kMetaEntries = size_t{1} << 16;
@@ -375,12 +381,12 @@ public:
             return kFallback;
         Slab* slab = nullptr;
         for (;;) {
-            for (Slab& s : slabs_)
+            for (Slab& s : active())
                 if (s.state == Slab::kOpen && s.matches(op, len) && s.reserved < s.capacity) slab = &s;
             if (!slab) {
-                for (Slab& s : slabs_)  // a different shape or a full arena closes the open batch
+                for (Slab& s : active())  // a different shape or a full arena closes the open batch
                     if (s.state == Slab::kOpen) s.full = true;
-                for (Slab& s : slabs_)
+                for (Slab& s : active())
                     if (s.state == Slab::kFree) {
                         s.open(op, len, pitch, tiles, arena_, ++opened_);
                         slab = &s;
@@ -508,7 +514,8 @@ private:
     int init(size_t arena)
     {
         arena_ = arena;
-        for (Slab& s : slabs_) {
+        nslabs_ = batch_config().slabs.load();
+        for (Slab& s : active()) {
             s.owner = this;
             hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming);
@@ -532,7 +539,7 @@ private:
     // Frees whatever init() allocated (after a failed init: nothing is in flight).
     void release()
     {
-        for (Slab& s : slabs_) {
+        for (Slab& s : active()) {
             if (s.stream) (void)hipStreamDestroy(s.stream);
             if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
             for (uint8_t* h : {s.pin_in, s.pin_out})
@@ -566,7 +573,7 @@ private:
             Slab* s = nullptr;
             cv_worker_.wait(lock, [&] {
                 s = nullptr;
-                for (Slab& x : slabs_)
+                for (Slab& x : active())
                     if (x.state == Slab::kOpen && (!s || x.seq < s->seq)) s = &x;
                 return s != nullptr;
             });
@@ -671,7 +678,15 @@ private:
     bool init_failed_ = false;  // the arenas could not be allocated: every call runs directly
     size_t arena_ = 0;
     uint64_t opened_ = 0;
-    Slab slabs_[kSlabs];
+    Slab slabs_[kMaxSlabs];
+    int nslabs_ = 3;  // set once by init()
+    struct SlabRange {
+        Slab* b;
+        Slab* e;
+        Slab* begin() const { return b; }
+        Slab* end() const { return e; }
+    };
+    SlabRange active() { return SlabRange{slabs_, slabs_ + nslabs_}; }
 };
 
 Batcher* batcher(int dev)

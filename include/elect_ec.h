@@ -99,11 +99,11 @@ int elect_ec_set_host_devices(const int* devices, int n);
  * returns only when its own outputs are written.  Dispatch is self-clocking: a
  * batch leaves when the previous batch's inputs are on the device (at once on
  * an idle device, or after window_us if non-zero), so transfers pipeline.
- * arena_bytes (per direction, x2 arenas, per device) takes effect for devices
+ * arena_bytes (per direction, x3 arenas by default, ELECT_EC_BATCH_SLABS, per device) takes effect for devices
  * whose batcher has not started yet.  ELECT issues up to concurrent_ec (64)
- * such calls at once (conf/elect.yaml:598): there batching measured 3x the
- * per-thread path (40.7 vs 12.5 GiB/s on 4.4 MB stripes); a lone caller loses
- * ~10 % (12.5 vs 13.7 GiB/s), as its stripe is not split into overlapped chunks. */
+ * such calls at once (conf/elect.yaml:598): there batching measured 4x the
+ * per-thread path (46-50 vs 12.5 GiB/s on 4.4 MB stripes); a lone caller runs
+ * at the per-thread path's rate (11.5-14 GiB/s). */
 int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes);
 
 /* ---- coder lifecycle ----

@@ -107,6 +107,12 @@ for step in "$@"; do
             lib=""; [ $v = a ] || lib="$PWD/elect_amd/_ab/libelect_ec_$v.so"
             ELECT_EC_LIB=$lib ELECT_EC_BATCH_TILE_KB=$tk run "bench_hostpath_${v}_tile${tk}_T${T}_$i" 300 python bench.py --config hostpath --threads $T --host-op ${HOST_OP:-encode} || exit $?
         done; done; done; done ;;
+    hostslabs)  # batcher arenas x arena size at 64 callers, ELECT's codeLength, interleaved 3x
+        IFS=';' read -ra CFGS <<< "${SLAB_CFGS:-2 256;3 256;4 256;2 512;3 512}"
+        for i in 1 2 3; do for c in "${CFGS[@]}"; do
+            set -- $c
+            ELECT_EC_BATCH_SLABS=$1 ELECT_EC_BATCH_ARENA_MB=$2 run "bench_hostpath_s$1_a$2_T${T:-64}_$i" 300 python bench.py --config hostpath --threads ${T:-64} --host-op ${HOST_OP:-encode} || exit $?
+        done; done ;;
     hostsweep) run hostsweep 600 python tools/tune/host_sweep.py || exit $? ;;
     copysizes) run copysizes 600 python tools/tune/host_sweep.py copysizes || exit $? ;;
     staged)
