@@ -410,7 +410,10 @@ def alloc_stripes(args, B: int, L: int, k: int, m: int, dev, generator=None):
 
 def timed(step, steps, warmup, world):
     """Warm up, then time exactly `steps` steps between barrier + synchronize on
-    both sides.  Returns (max over ranks of the elapsed seconds, this rank's host
+    both sides.  Each rank's clock starts when the opening barrier releases it
+    and stops at its closing synchronize (the closing gloo barrier costs ~0.6 ms
+    at 8 ranks, a few % of a 20-step region, and is no part of a step); the
+    max over ranks is the job's time.  Returns (max over ranks of the elapsed seconds, this rank's host
     submit time per step in ms: the time the host spends issuing one step's
     launches, which must stay well below the step's GPU time)."""
     for _ in range(warmup):
@@ -425,8 +428,9 @@ def timed(step, steps, warmup, world):
         step()
         submit += time.perf_counter() - s0
     torch.cuda.synchronize()
+    own = time.perf_counter() - t0  # this rank's steps, up to its own synchronize
     barrier(world)
-    return max_over_ranks(time.perf_counter() - t0, world), submit / steps * 1e3
+    return max_over_ranks(own, world), submit / steps * 1e3
 
 
 def graph_steps(fns):
@@ -1074,8 +1078,8 @@ def main():
         step(evs[i])
         submit += time.perf_counter() - s0
     torch.cuda.synchronize()
-    barrier(world)
-    own = time.perf_counter() - t0
+    own = time.perf_counter() - t0  # clock stops at this rank's synchronize; the
+    barrier(world)                  # closing barrier's own latency is not a step's
     elapsed = max_over_ranks(own, world)
     submit_ms = submit / args.steps * 1e3
 
