@@ -99,6 +99,9 @@ def parse():
                     help="mixed: issue the size classes on this many streams (1: one stream, in order)")
     ap.add_argument("--mixed-share", type=int, default=0,
                     help="mixed: code rank 0's share of an N-rank partition on this GPU (strong-scaling probe)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="headline: issue step i (its batch's encode + decode) on stream i %% S; with "
+                         "S > 1 consecutive steps' kernels may overlap at their boundaries")
     ap.add_argument("--graph", action="store_true",
                     help="headline and mixed: capture each step's launches in a HIP graph and replay it")
     ap.add_argument("--launch-check", action="store_true",
@@ -1050,8 +1053,18 @@ def main():
     ops = [(encode_of(st), decode_of(st, rb)) for st, rb in sets]
     replays = graph_steps([lambda e=e, d=d: (e(), d()) for e, d in ops]) if args.graph else None
 
+    lanes = [torch.cuda.Stream() for _ in range(args.streams)] if args.streams > 1 else None
+    if lanes is not None and (replays is not None or len(sets) % args.streams):
+        raise SystemExit("--streams S needs eager launches and --rotate a multiple of S")
+
     def step(ev=None):
         i = turn[0] % len(sets)
+        if lanes is not None and ev is None:  # batch i always on lane i % S: reuse stays ordered
+            turn[0] += 1
+            with torch.cuda.stream(lanes[i % len(lanes)]):
+                ops[i][0]()
+                ops[i][1]()
+            return
         turn[0] += 1
         if ev is not None:
             ev[0].record(stream)
@@ -1075,7 +1088,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         s0 = time.perf_counter()
-        step(evs[i])
+        step(evs[i] if lanes is None else None)
         submit += time.perf_counter() - s0
     torch.cuda.synchronize()
     own = time.perf_counter() - t0  # clock stops at this rank's synchronize; the
@@ -1083,7 +1096,7 @@ def main():
     elapsed = max_over_ranks(own, world)
     submit_ms = submit / args.steps * 1e3
 
-    if replays is not None:  # per-kernel split from an eager pass (a graph replay is one span)
+    if replays is not None or lanes is not None:  # per-kernel split from an eager one-stream pass
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
         replays, keep = None, replays
         for i in range(args.steps):
@@ -1126,6 +1139,7 @@ def main():
             "rotate": args.rotate,  # disjoint batches per rank, one per step in turn
             "parallelism": f"stripe-partitioned x{world}, no collectives (gloo timing handshake only)",
             "graph": bool(args.graph),
+            "streams": args.streams,
         },
         "host_submit_ms_per_step": round(submit_ms, 4),
         "roofline": {
