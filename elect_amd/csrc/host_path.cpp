@@ -59,6 +59,115 @@ void stream_copy(uint8_t* dst, const uint8_t* src, size_t n)
     std::memcpy(dst, src, n);
 }
 
+// Copy fan-out for lone callers.  One thread's staging copies (~20 GB/s) bound a
+// caller that has the device to itself: a 4.4 MB RS(6,4) stripe moves 26 MB
+// through them against 0.5 ms of DMA.  Such a caller spreads its copies over a
+// few helper threads (ELECT_EC_COPY_THREADS, default 8; 0 disables); with many
+// callers in flight every caller copies its own, as the cores are busy anyway.
+struct CopyJob {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t n;
+};
+
+// Appends dst <- src[0, n) as pieces of at most 1 MiB.
+void add_copy(std::vector<CopyJob>& jobs, uint8_t* dst, const uint8_t* src, size_t n)
+{
+    constexpr size_t kPiece = size_t{1} << 20;
+    for (size_t o = 0; o < n; o += kPiece) jobs.push_back(CopyJob{dst + o, src + o, std::min(kPiece, n - o)});
+}
+
+class CopyPool {
+public:
+    static CopyPool* get()
+    {
+        static CopyPool* pool = [] {
+            const char* e = std::getenv("ELECT_EC_COPY_THREADS");
+            const int n = e ? std::min(16, std::max(0, std::atoi(e))) : 8;
+            return n > 0 ? new (std::nothrow) CopyPool(n) : nullptr;  // never destroyed: helpers live until exit
+        }();
+        return pool;
+    }
+
+    // Runs the jobs on this thread and the helpers, and returns once all are
+    // done and their streamed stores fenced.  False (nothing copied) when another
+    // caller holds the pool.
+    bool run(const std::vector<CopyJob>& jobs)
+    {
+        bool idle = false;
+        if (!busy_.compare_exchange_strong(idle, true)) return false;
+        {
+            std::lock_guard<std::mutex> lock(mu_);
+            jobs_ = jobs.data();
+            njobs_ = jobs.size();
+            next_.store(0);
+            ++gen_;
+        }
+        cv_go_.notify_all();
+        drain(jobs.data(), jobs.size());
+        _mm_sfence();
+        {
+            // every job is claimed; wait for the helpers that joined to finish theirs
+            std::unique_lock<std::mutex> lock(mu_);
+            cv_done_.wait(lock, [&] { return working_ == 0; });
+            jobs_ = nullptr;  // helpers waking from here on find nothing to join
+        }
+        busy_.store(false);
+        return true;
+    }
+
+private:
+    explicit CopyPool(int n)
+    {
+        for (int i = 0; i < n; ++i) std::thread(&CopyPool::helper, this).detach();
+    }
+
+    void drain(const CopyJob* jobs, size_t n)
+    {
+        for (size_t i = next_.fetch_add(1); i < n; i = next_.fetch_add(1)) stream_copy(jobs[i].dst, jobs[i].src, jobs[i].n);
+    }
+
+    void helper()
+    {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lock(mu_);
+        for (;;) {
+            cv_go_.wait(lock, [&] { return gen_ != seen; });
+            seen = gen_;
+            if (!jobs_) continue;  // that job is over
+            const CopyJob* jobs = jobs_;
+            const size_t n = njobs_;
+            ++working_;
+            lock.unlock();
+            drain(jobs, n);
+            _mm_sfence();  // this thread's streamed stores, before the caller hands the data on
+            lock.lock();
+            if (--working_ == 0) cv_done_.notify_one();
+        }
+    }
+
+    std::atomic<bool> busy_{false};
+    std::mutex mu_;
+    std::condition_variable cv_go_, cv_done_;
+    const CopyJob* jobs_ = nullptr;  // the current job, under mu_
+    size_t njobs_ = 0;
+    uint64_t gen_ = 0;
+    int working_ = 0;  // helpers inside the current job
+    std::atomic<size_t> next_{0};
+};
+
+// Runs the copies through the pool when the caller is (nearly) alone and the
+// copies are large enough to split, else on this thread.
+void run_copies(const std::vector<CopyJob>& jobs, bool lone)
+{
+    size_t bytes = 0;
+    for (const CopyJob& j : jobs) bytes += j.n;
+    CopyPool* pool = lone && bytes >= (size_t{2} << 20) && jobs.size() > 1 ? CopyPool::get() : nullptr;
+    if (pool && pool->run(jobs)) return;
+    for (const CopyJob& j : jobs) stream_copy(j.dst, j.src, j.n);
+    _mm_sfence();  // the streamed stores are visible before the data is handed on
+}
+
 // ---------------------------------------------------------------------------
 // Host-memory path: per-thread, per-device staging engine.
 // Input chunks are copied into pinned buffers, sent H2D, coded, returned D2H
@@ -236,6 +345,7 @@ private:
 
 constexpr int kMaxDevices = 64;
 thread_local std::unique_ptr<HostEngine> t_engines[kMaxDevices];
+thread_local std::vector<CopyJob> t_jobs;  // a caller's staging copies (Batcher::submit)
 
 // Device policy of the host-memory path (elect_ec_set_host_devices).
 struct DevicePolicy {
@@ -356,11 +466,18 @@ public:
     // Per-slot content lengths (padded ops) and parity hashes (hashed ops) of a
     // batch: entries per arena, which caps such a batch's stripes.
     static constexpr size_t kMetaEntries = size_t{1} << 16;
+    // A caller fans its copies out (CopyPool) while at most this many callers are in flight.
+    static constexpr int kLoneCallers = 2;
 
     explicit Batcher(int dev) : dev_(dev) {}
 
     int submit(const HostOp& op, size_t len)
     {
+        struct InFlight {  // callers inside submit(), for the copy fan-out policy
+            std::atomic<int>& n;
+            explicit InFlight(std::atomic<int>& c) : n(c) { n.fetch_add(1); }
+            ~InFlight() { n.fetch_sub(1); }
+        } in_flight(callers_);
         // untiled: one unit per column at a 256-byte pitch; tiled: T tiles of 64 KiB
         const size_t tile = batch_config().tile.load();
         const size_t tiles = tile && tile % 16 == 0 && len > tile ? (len + tile - 1) / tile : 1;
@@ -406,13 +523,15 @@ public:
         // tile t of column j at slot * in_stride + (t * cols + j) * pitch (untiled: t = 0)
         const size_t in_stride = tiles * op.cols * pitch;  // == the slab's (matches())
         uint8_t* const in_base = slab->pin_in + slot * in_stride;
+        std::vector<CopyJob>& jobs = t_jobs;
+        jobs.clear();
         for (int j = 0; j < op.cols; ++j) {
             const size_t n = op.lens ? op.lens[j] : len;  // padded: only the content bytes
             if (op.lens) slab->pin_lens[static_cast<size_t>(slot) * op.cols + j] = static_cast<uint32_t>(n);
             for (size_t o = 0; o < n; o += pitch)  // untiled: pitch >= len, one copy
-                stream_copy(in_base + (o / pitch * op.cols + j) * pitch, op.in[j] + o, std::min(pitch, n - o));
+                add_copy(jobs, in_base + (o / pitch * op.cols + j) * pitch, op.in[j] + o, std::min(pitch, n - o));
         }
-        _mm_sfence();  // the streamed stores are visible before the dispatcher's H2D reads them
+        run_copies(jobs, callers_.load() <= kLoneCallers);  // fenced before the dispatcher's H2D reads them
 
         lock.lock();
         if (++slab->filled == slab->reserved) cv_worker_.notify_one();
@@ -423,12 +542,14 @@ public:
         if (status == ELECT_EC_OK) {
             const size_t out_stride = tiles * op.rows * pitch;
             const uint8_t* const out_base = slab->pin_out + slot * out_stride;
+            jobs.clear();
             for (int r = 0; r < op.rows; ++r)
                 for (size_t t = 0; t < tiles; ++t) {
                     const size_t o = t * pitch;
-                    stream_copy(op.out[r] + o, out_base + (t * op.rows + r) * pitch, tiles > 1 ? std::min(pitch, len - o) : len);
+                    add_copy(jobs, op.out[r] + o, out_base + (t * op.rows + r) * pitch,
+                             tiles > 1 ? std::min(pitch, len - o) : len);
                 }
-            _mm_sfence();
+            run_copies(jobs, callers_.load() <= kLoneCallers);
             if (op.hashes)
                 std::memcpy(op.hashes, slab->pin_hash + static_cast<size_t>(slot) * op.rows, op.rows * sizeof(int32_t));
         }
@@ -668,6 +789,7 @@ private:
     }
 
     int dev_;
+    std::atomic<int> callers_{0};
     // One mutex; three kinds of waiter, so that a state change wakes only the
     // threads it concerns (one condition variable for all woke every caller on
     // every reservation: O(callers^2) wake-ups per batch at 64 callers).

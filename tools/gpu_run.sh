@@ -113,6 +113,14 @@ for step in "$@"; do
             set -- $c
             ELECT_EC_BATCH_SLABS=$1 ELECT_EC_BATCH_ARENA_MB=$2 run "bench_hostpath_s$1_a$2_T${T:-64}_$i" 300 python bench.py --config hostpath --threads ${T:-64} --host-op ${HOST_OP:-encode} || exit $?
         done; done ;;
+    copythreads)  # lone-caller copy fan-out: ELECT_EC_COPY_THREADS x callers, ELECT's codeLength, interleaved 3x
+        for i in 1 2 3; do for ct in ${COPY_CFGS:-0 4 8}; do for T in ${T_LIST:-1 2 64}; do
+            ELECT_EC_COPY_THREADS=$ct run "bench_hostpath_ct${ct}_T${T}_$i" 300 python bench.py --config hostpath --threads $T --host-op ${HOST_OP:-encode} || exit $?
+        done; done; done ;;
+    tsan)  # the host stress under ThreadSanitizer (built here first: SANITIZER=tsan tools/sanitize/run.sh build)
+        SANITIZER=tsan run tsan_stress 600 bash tools/sanitize/run.sh run ${TSAN_T:-8} ${TSAN_N:-4} || exit $? ;;
+    asan)  # the host stress under ASan + UBSan
+        run asan_stress 600 bash tools/sanitize/run.sh run || exit $? ;;
     hostsweep) run hostsweep 600 python tools/tune/host_sweep.py || exit $? ;;
     copysizes) run copysizes 600 python tools/tune/host_sweep.py copysizes || exit $? ;;
     staged)

@@ -41,12 +41,13 @@ static int32_t java_hash(const uint8_t* p, size_t n)
         }                                               \
     } while (0)
 
-static void worker(const elect_ec_coder* c, int k, int m, int tid, int iters)
+static void worker(const elect_ec_coder* c, int k, int m, int tid, int iters, size_t big = 0)
 {
     std::mt19937_64 rng(1000 + tid);
     auto rnd = [&](size_t lo, size_t hi) { return lo + rng() % (hi - lo + 1); };
     for (int it = 0; it < iters; ++it) {
-        const size_t L = rng() % 4 == 0 ? rnd(1, 64) : rnd(1000, 300000);
+        // big: units of big/3..big bytes, so that a lone caller's copies fan out (CopyPool)
+        const size_t L = big ? rnd(big / 3, big) : rng() % 4 == 0 ? rnd(1, 64) : rnd(1000, 300000);
         std::vector<std::vector<uint8_t>> d(k, std::vector<uint8_t>(L)), p(m, std::vector<uint8_t>(L));
         std::vector<size_t> lens(k);
         for (int j = 0; j < k; ++j) {
@@ -192,10 +193,19 @@ int main(int argc, char** argv)
         if (batching > first) continue;
         elect_ec_set_batching(batching, 0, size_t{8} << 20);  // small arenas: batches close often
         std::vector<std::thread> th;
-        for (int t = 0; t < threads; ++t) th.emplace_back(worker, c, 4, 2, t + 100 * batching, iters);
+        for (int t = 0; t < threads; ++t) th.emplace_back(worker, c, 4, 2, t + 100 * batching, iters, size_t{0});
         for (auto& x : th) x.join();
         std::printf("batching=%d: %d threads x %d iterations, failures so far %d\n", batching, threads, iters,
                     g_fail.load());
+    }
+    {  // one and two callers on multi-MB stripes: the copy fan-out, and two callers racing for it
+        elect_ec_set_batching(1, 0, size_t{8} << 20);
+        for (int n : {1, 2}) {
+            std::vector<std::thread> th;
+            for (int t = 0; t < n; ++t) th.emplace_back(worker, c, 4, 2, t + 200 + 10 * n, iters, size_t{1900000});
+            for (auto& x : th) x.join();
+        }
+        std::printf("lone callers: 1 and 2 threads x %d iterations, failures so far %d\n", iters, g_fail.load());
     }
     {
         std::vector<std::thread> th;
