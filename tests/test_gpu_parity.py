@@ -731,3 +731,60 @@ def test_encode_decode_batches_equal_per_batch_calls(dev, oracle, k, m):
     for st, o in zip(stripes, outs):
         for q, e in enumerate(erased):
             assert torch.equal(o[:, q], st[:, e])
+
+
+@pytest.mark.parametrize("helpers", ["0", "1", "16"])
+def test_lone_caller_copy_fanout(dev, helpers):
+    """The batcher's copy fan-out (host_path.cpp CopyPool: a caller with at most
+    one other call in flight shares its staging copies with helper threads):
+    one caller, then two racing for the pool, on ELECT's codeLength and a 2 MB
+    unit, through encode_ex (padded + hashed), decode_ex and encode_update_ex;
+    bit-exact against the oracle with the pool off (0), minimal (1) and widest (16)."""
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    code = f"""
+import sys, threading, numpy as np
+sys.path.insert(0, {ROOT!r})
+from elect_amd.coder import RSCoder
+from oracle import ec_oracle
+k, m = 4, 2
+c = RSCoder(k, m)
+enc = ec_oracle.Encoder(k, m)
+bad = []
+
+def one(seed, L):
+    rng = np.random.default_rng(seed)
+    d = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    lens = [L, L - 1000 - seed % 7, L // 3, 0]
+    z = [np.where(np.arange(L) < n, x, 0).astype(np.uint8) for x, n in zip(d, lens)]
+    p = [np.empty(L, np.uint8) for _ in range(m)]
+    hs = c.encode_ex_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L, data_lengths=lens, hashed=True)
+    want = enc.encode(z)
+    if not all(np.array_equal(a, b) for a, b in zip(p, want)) or hs != [ec_oracle.java_hashcode(w) for w in want]:
+        bad.append(("encode_ex", seed, L))
+    out = [np.empty(L, np.uint8)]
+    c.decode_ex_host([z[1].ctypes.data, z[2].ctypes.data, z[3].ctypes.data, p[0].ctypes.data], [1, 2, 3, 4], [0],
+                     [x.ctypes.data for x in out], L)
+    if not np.array_equal(out[0], z[0]):
+        bad.append(("decode_ex", seed, L))
+    new = rng.integers(0, 256, L, dtype=np.uint8)
+    q = [np.empty(L, np.uint8) for _ in range(m)]
+    c.encode_update_ex_host([z[2].ctypes.data, new.ctypes.data, p[0].ctypes.data, p[1].ctypes.data], 2,
+                            [x.ctypes.data for x in q], L)
+    z[2] = new
+    if not all(np.array_equal(a, b) for a, b in zip(q, enc.encode(z))):
+        bad.append(("update", seed, L))
+
+for L in (4404020, 2 << 20):
+    one(1, L)  # a lone caller
+    th = [threading.Thread(target=one, args=(s, L)) for s in (2, 3)]  # two callers racing for the pool
+    [t.start() for t in th]
+    [t.join() for t in th]
+print("bad", bad)
+assert not bad
+print("fanout ok")
+"""
+    env = dict(__import__("os").environ, ELECT_EC_COPY_THREADS=helpers)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0 and "fanout ok" in r.stdout, r.stdout + r.stderr
