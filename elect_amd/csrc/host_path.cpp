@@ -466,8 +466,16 @@ public:
     // Per-slot content lengths (padded ops) and parity hashes (hashed ops) of a
     // batch: entries per arena, which caps such a batch's stripes.
     static constexpr size_t kMetaEntries = size_t{1} << 16;
-    // A caller fans its copies out (CopyPool) while at most this many callers are in flight.
-    static constexpr int kLoneCallers = 2;
+    // A caller fans its copies out (CopyPool) while at most this many callers are
+    // in flight (ELECT_EC_COPY_FANOUT_CALLERS, default 2).
+    static int lone_callers()
+    {
+        static const int n = [] {
+            const char* e = std::getenv("ELECT_EC_COPY_FANOUT_CALLERS");
+            return e ? std::max(0, std::atoi(e)) : 2;
+        }();
+        return n;
+    }
 
     explicit Batcher(int dev) : dev_(dev) {}
 
@@ -531,7 +539,7 @@ public:
             for (size_t o = 0; o < n; o += pitch)  // untiled: pitch >= len, one copy
                 add_copy(jobs, in_base + (o / pitch * op.cols + j) * pitch, op.in[j] + o, std::min(pitch, n - o));
         }
-        run_copies(jobs, callers_.load() <= kLoneCallers);  // fenced before the dispatcher's H2D reads them
+        run_copies(jobs, callers_.load() <= lone_callers());  // fenced before the dispatcher's H2D reads them
 
         lock.lock();
         if (++slab->filled == slab->reserved) cv_worker_.notify_one();
@@ -549,7 +557,7 @@ public:
                     add_copy(jobs, op.out[r] + o, out_base + (t * op.rows + r) * pitch,
                              tiles > 1 ? std::min(pitch, len - o) : len);
                 }
-            run_copies(jobs, callers_.load() <= kLoneCallers);
+            run_copies(jobs, callers_.load() <= lone_callers());
             if (op.hashes)
                 std::memcpy(op.hashes, slab->pin_hash + static_cast<size_t>(slot) * op.rows, op.rows * sizeof(int32_t));
         }

@@ -115,7 +115,7 @@ for step in "$@"; do
         done; done ;;
     copythreads)  # lone-caller copy fan-out: ELECT_EC_COPY_THREADS x callers, ELECT's codeLength, interleaved 3x
         for i in 1 2 3; do for ct in ${COPY_CFGS:-0 4 8}; do for T in ${T_LIST:-1 2 64}; do
-            ELECT_EC_COPY_THREADS=$ct run "bench_hostpath_ct${ct}_T${T}_$i" 300 python bench.py --config hostpath --threads $T --host-op ${HOST_OP:-encode} || exit $?
+            ELECT_EC_COPY_THREADS=$ct ELECT_EC_COPY_FANOUT_CALLERS=${FANOUT:-2} run "bench_hostpath_ct${ct}_f${FANOUT:-2}_T${T}_$i" 300 python bench.py --config hostpath --threads $T --host-op ${HOST_OP:-encode} || exit $?
         done; done; done ;;
     tsan)  # the host stress under ThreadSanitizer (built here first: SANITIZER=tsan tools/sanitize/run.sh build)
         SANITIZER=tsan run tsan_stress 600 bash tools/sanitize/run.sh run ${TSAN_T:-8} ${TSAN_N:-4} || exit $? ;;
