@@ -217,6 +217,26 @@ int update_batch_impl(const elect_ec_coder* coder, size_t chunk_size, size_t til
     return map_hip(elect::kern::launch_apply(p, as_stream(stream)));
 }
 
+// The batches calls' parameter list and grouped launch, with allocation
+// failures as status codes (nothing unwinds through the C ABI).
+bool reserve_params(std::vector<ApplyParams>& ps, int n)
+{
+    try {
+        ps.resize(static_cast<size_t>(n));
+        return true;
+    } catch (const std::bad_alloc&) {
+        return false;
+    }
+}
+
+int apply_many(const std::vector<ApplyParams>& ps, int n, void* stream)
+{
+    try {
+        return map_hip(elect::kern::launch_apply_many(ps.data(), n, as_stream(stream)));
+    } catch (const std::bad_alloc&) {
+        return ELECT_EC_ENOMEM;
+    }
+}
 }  // namespace
 
 extern "C" {
@@ -577,7 +597,8 @@ int elect_ec_encode_batches(const elect_ec_coder* coder, const elect_ec_batch* b
                             void* stream)
 {
     if (!valid_coder(coder) || num_batches < 0 || (num_batches > 0 && !batches)) return ELECT_EC_EINVAL;
-    std::vector<ApplyParams> ps(static_cast<size_t>(num_batches));
+    std::vector<ApplyParams> ps;
+    if (!reserve_params(ps, num_batches)) return ELECT_EC_ENOMEM;
     for (int i = 0; i < num_batches; ++i) {
         const elect_ec_batch& b = batches[i];
         if (b.chunk_size && b.num_stripes && (!b.in.base || !b.out.base)) return ELECT_EC_EINVAL;
@@ -592,7 +613,7 @@ int elect_ec_encode_batches(const elect_ec_coder* coder, const elect_ec_batch* b
             std::memcpy(p.coef + r * p.cols, parity_row(coder, r), coder->k);
         }
     }
-    return map_hip(elect::kern::launch_apply_many(ps.data(), num_batches, as_stream(stream)));
+    return apply_many(ps, num_batches, stream);
 }
 
 int elect_ec_decode_batches(const elect_ec_coder* coder, const elect_ec_batch* batches, int num_batches,
@@ -604,7 +625,8 @@ int elect_ec_decode_batches(const elect_ec_coder* coder, const elect_ec_batch* b
     const int st = build_decode_matrix(coder, decode_indexes, erased_indexes, num_erased, mode, coef);
     if (st < 0) return st;
     if (num_erased == 0) return st;
-    std::vector<ApplyParams> ps(static_cast<size_t>(num_batches));
+    std::vector<ApplyParams> ps;
+    if (!reserve_params(ps, num_batches)) return ELECT_EC_ENOMEM;
     for (int i = 0; i < num_batches; ++i) {
         const elect_ec_batch& b = batches[i];
         if (b.chunk_size && b.num_stripes && (!b.in.base || !b.out.base)) return ELECT_EC_EINVAL;
@@ -623,7 +645,7 @@ int elect_ec_decode_batches(const elect_ec_coder* coder, const elect_ec_batch* b
             p.dst[r] = col(b.out.base, b.out.stripe_stride, slot * b.out.shard_stride);
         }
     }
-    const int rc = map_hip(elect::kern::launch_apply_many(ps.data(), num_batches, as_stream(stream)));
+    const int rc = apply_many(ps, num_batches, stream);
     return rc != ELECT_EC_OK ? rc : st;
 }
 

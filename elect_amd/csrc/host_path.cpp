@@ -119,7 +119,10 @@ public:
 private:
     explicit CopyPool(int n)
     {
-        for (int i = 0; i < n; ++i) std::thread(&CopyPool::helper, this).detach();
+        try {
+            for (int i = 0; i < n; ++i) std::thread(&CopyPool::helper, this).detach();
+        } catch (...) {  // fewer helpers (or none: callers then drain their jobs alone)
+        }
     }
 
     void drain(const CopyJob* jobs, size_t n)
@@ -490,6 +493,11 @@ public:
         const size_t tile = batch_config().tile.load();
         const size_t tiles = tile && tile % 16 == 0 && len > tile ? (len + tile - 1) / tile : 1;
         const size_t pitch = tiles > 1 ? tile : (len + 255) & ~size_t{255};
+        // the copy lists' room first: past the reservation below nothing may throw
+        // (a slot reserved and never filled would stall its batch)
+        std::vector<CopyJob>& jobs = t_jobs;
+        jobs.clear();
+        jobs.reserve(static_cast<size_t>(std::max(op.cols, op.rows)) * (tiles + (len >> 20) + 1));
         std::unique_lock<std::mutex> lock(mu_);
         if (init_failed_) return kFallback;
         if (!started_) {  // arenas, streams and events once, before anything is in flight
@@ -499,7 +507,13 @@ public:
                 init_failed_ = true;
                 return kFallback;
             }
-            std::thread(&Batcher::worker, this).detach();  // lives as long as the process
+            try {
+                std::thread(&Batcher::worker, this).detach();  // lives as long as the process
+            } catch (...) {  // no dispatcher: the per-thread engine serves every call
+                release();
+                init_failed_ = true;
+                return kFallback;
+            }
             started_ = true;
         }
         if (static_cast<size_t>(op.cols) * pitch * tiles > arena_ || static_cast<size_t>(op.rows) * pitch * tiles > arena_)
@@ -531,8 +545,6 @@ public:
         // tile t of column j at slot * in_stride + (t * cols + j) * pitch (untiled: t = 0)
         const size_t in_stride = tiles * op.cols * pitch;  // == the slab's (matches())
         uint8_t* const in_base = slab->pin_in + slot * in_stride;
-        std::vector<CopyJob>& jobs = t_jobs;
-        jobs.clear();
         for (int j = 0; j < op.cols; ++j) {
             const size_t n = op.lens ? op.lens[j] : len;  // padded: only the content bytes
             if (op.lens) slab->pin_lens[static_cast<size_t>(slot) * op.cols + j] = static_cast<uint32_t>(n);
@@ -842,21 +854,31 @@ int run_host(const HostOp& op, size_t len)
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return ELECT_EC_ENODEV;
     int dev = 0;
-    int rc = host_device(ndev, &dev);
+    int rc = ELECT_EC_ENOMEM;
+    try {
+        rc = host_device(ndev, &dev);  // (parses ELECT_EC_DEVICES on first use)
+    } catch (...) {
+    }
     if (rc != ELECT_EC_OK) return rc;
     if (dev < 0 || dev >= kMaxDevices || dev >= ndev) return ELECT_EC_ENODEV;
     int prev = 0;
     hipError_t e = hipGetDevice(&prev);
     if (e == hipSuccess && prev != dev) e = hipSetDevice(dev);
     if (e != hipSuccess) return map_hip(e);
-    rc = Batcher::kFallback;
-    if (batch_config().enabled.load() == 1) {
-        Batcher* b = batcher(dev);
-        rc = b ? b->submit(op, len) : ELECT_EC_ENOMEM;
-    }
-    if (rc == Batcher::kFallback) {
-        if (!t_engines[dev]) t_engines[dev].reset(new (std::nothrow) HostEngine(dev));
-        rc = t_engines[dev] ? t_engines[dev]->run(op, len) : ELECT_EC_ENOMEM;
+    try {  // nothing may unwind into the JVM: allocation failures become status codes
+        rc = Batcher::kFallback;
+        if (batch_config().enabled.load() == 1) {
+            Batcher* b = batcher(dev);
+            rc = b ? b->submit(op, len) : ELECT_EC_ENOMEM;
+        }
+        if (rc == Batcher::kFallback) {
+            if (!t_engines[dev]) t_engines[dev].reset(new (std::nothrow) HostEngine(dev));
+            rc = t_engines[dev] ? t_engines[dev]->run(op, len) : ELECT_EC_ENOMEM;
+        }
+    } catch (const std::bad_alloc&) {
+        rc = ELECT_EC_ENOMEM;
+    } catch (...) {  // std::system_error: a thread could not be started
+        rc = ELECT_EC_ENOMEM;
     }
     if (prev != dev) (void)hipSetDevice(prev);  // the caller's current device is left as it was
     return rc;
@@ -872,7 +894,12 @@ int set_host_devices(const int* devices, int n)
     DevicePolicy& p = policy();
     std::lock_guard<std::mutex> lock(p.mu);
     p.env_read = true;  // an explicit list overrides the environment
-    p.devices.assign(devices, devices + n);
+    try {
+        p.devices.assign(devices, devices + n);
+    } catch (const std::bad_alloc&) {
+        p.devices.clear();
+        return ELECT_EC_ENOMEM;
+    }
     p.next = 0;
     p.generation++;  // threads pick a device again on their next call
     return ELECT_EC_OK;
