@@ -70,6 +70,8 @@ def parse():
                     help="target CPU-baseline work time (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (PCIe) measurement")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the mixed (configs[3]) and RS(12,8) (configs[4]) lines of the headline run")
     ap.add_argument("--no-sizes", action="store_true",
                     help="headline: skip the 1 KiB / 1 MiB chunk-size lines (sizes) after the 64 KiB one")
     ap.add_argument("--config", default="headline",
@@ -960,6 +962,25 @@ def config_flows(args, world, rank, dev):
                        "parallelism": f"stripe-partitioned x{world}"}}
 
 
+def other_configs(args, world, rank, dev):
+    """The mixed (strong-scaled) and RS(12,8) (weak-scaled) configs inside the
+    headline run, so every `--gpus N` line the driver records carries all three
+    multi-GPU BASELINE configs at that N.  Same timing as their own --config
+    runs (barrier + synchronize both sides, max over ranks), 20 steps."""
+    import copy
+    sub = copy.copy(args)
+    sub.steps, sub.warmup, sub.mixed_share = min(args.steps, 20), min(args.warmup, 3), 0
+    res = {}
+    for name, fn in (("mixed", config_mixed), ("rs12", config_rs12)):
+        o = fn(sub, world, rank, dev)
+        keep = ("metric", "value", "unit", "scaling", "steps", "ms_per_step", "host_submit_ms_per_step",
+                "verified", "classes", "kernels")
+        res[name] = {key: o[key] for key in keep if key in o}
+        res[name]["workload"] = o["config"]["workload"]
+        torch.cuda.empty_cache()
+    return res
+
+
 def launch_check(args, world, rank):
     """--launch-check: the multi-rank plumbing with no GPU work (CPU test)."""
     barrier(world)
@@ -1177,6 +1198,11 @@ def main():
         rec["sizes_verified"] = all(v["verified"] for v in out["sizes"].values())
         rec["sizes_submit_ms"] = {key: v["host_submit_ms_per_step"] for key, v in out["sizes"].items()}
         rec["verified"] = rec["verified"] and rec["sizes_verified"]
+    if not args.no_configs:  # BASELINE configs[3] and [4] at the same N (every rank; own barriers)
+        out["configs"] = other_configs(args, world, rank, dev)
+        rec["configs_verified"] = {key: v["verified"] for key, v in out["configs"].items()}
+        rec["configs_submit_ms"] = {key: v["host_submit_ms_per_step"] for key, v in out["configs"].items()}
+        rec["verified"] = rec["verified"] and all(rec["configs_verified"].values())
     if rank == 0:
         out["kernels"]["decode_sweep"] = sw = decode_sweep(coder, stripe, k, m, L, B, stream)
         rec["verified"] = rec["verified"] and all(v["verified"] for v in sw.values())

@@ -1001,6 +1001,17 @@ constexpr std::array<FastFn, kFastRows> fast_row_fns()
             &launch_fast_kr<K, 4, PAD>};
 }
 
+// Grouped launches take every groupable batch of a call, whatever its chunk
+// size, in one launch of the smallest block size any part wants (block_for):
+// the mixed config's 8-way share 3,879 -> 3,959 GiB/s, 4-way 4,084 -> 4,116,
+// full size unchanged, against one launch per block-size class; one launch of
+// 256-thread blocks lost 5 % at full size (profiles/r02_group_ab/).
+// A/B builds: -DAB_GROUP_BLOCK=-1 restores one launch per class, 128 / 256 force a size.
+#ifndef AB_GROUP_BLOCK
+#define AB_GROUP_BLOCK 0
+#endif
+inline int group_class(const ApplyParams& p) { return AB_GROUP_BLOCK < 0 ? block_for(p.len, p.rows * p.cols) : 0; }
+
 const std::array<std::array<FastFn, kFastRows>, kMaxCols> kFast = {
     fast_row_fns<1>(),  fast_row_fns<2>(),  fast_row_fns<3>(),  fast_row_fns<4>(),
     fast_row_fns<5>(),  fast_row_fns<6>(),  fast_row_fns<7>(),  fast_row_fns<8>(),
@@ -1024,9 +1035,9 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
     a.n = n;
     for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(ps[0].coef[(r0 + r) * ps[0].cols + j]);
-    uint64_t len_max = 0;
-    for (int i = 0; i < n; ++i) len_max = std::max<uint64_t>(len_max, ps[i].len);
-    const int block = block_for(len_max, R * K);
+    int block = kBlock;
+    for (int i = 0; i < n; ++i) block = std::min(block, block_for(ps[i].len, R * K));
+    if (AB_GROUP_BLOCK > 0) block = AB_GROUP_BLOCK;
     uint64_t blocks = 0;
     for (int i = 0; i < n; ++i) {
         const ApplyParams& p = ps[i];
@@ -1450,15 +1461,15 @@ hipError_t launch_apply_many(const ApplyParams* ps, int n, hipStream_t stream)
         const hipError_t e = launch_apply_impl(p, stream);
         if (e != hipSuccess) return e;
     }
-    // Batches group with others of the same block-size class (block_for: small chunks
-    // run 128-thread blocks), in submission order within a class.
+    // Batches group in submission order (group_class: one class unless an A/B build
+    // splits them by block size).
     std::stable_sort(grouped.begin(), grouped.end(), [](const ApplyParams& x, const ApplyParams& y) {
-        return block_for(x.len, x.rows * x.cols) < block_for(y.len, y.rows * y.cols);
+        return group_class(x) < group_class(y);
     });
     for (size_t g0 = 0; g0 < grouped.size();) {
-        const int cls = block_for(grouped[g0].len, grouped[g0].rows * grouped[g0].cols);
+        const int cls = group_class(grouped[g0]);
         size_t g1 = g0 + 1;
-        while (g1 < grouped.size() && g1 - g0 < kMaxGroup && block_for(grouped[g1].len, grouped[g1].rows * grouped[g1].cols) == cls)
+        while (g1 < grouped.size() && g1 - g0 < kMaxGroup && group_class(grouped[g1]) == cls)
             ++g1;
         const int m = static_cast<int>(g1 - g0);
         if (m == 1) {  // nothing to group with: the plain launcher

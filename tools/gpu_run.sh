@@ -28,12 +28,12 @@ for step in "$@"; do
     bench) run bench 600 python bench.py || exit $? ;;
     prof)
         run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run \
-            -- python3 bench.py --no-cpu --no-host --no-sizes --steps 50 --warmup 5 || exit $? ;;
+            -- python3 bench.py --no-cpu --no-host --no-sizes --no-configs --steps 50 --warmup 5 || exit $? ;;
     pmc)
         run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_$TAG -o run \
-            -- python3 bench.py --no-cpu --no-host --no-sizes --steps 5 --warmup 1 || exit $?
+            -- python3 bench.py --no-cpu --no-host --no-sizes --no-configs --steps 5 --warmup 1 || exit $?
         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run \
-            -- python3 bench.py --no-cpu --no-host --no-sizes --steps 5 --warmup 1 || exit $? ;;
+            -- python3 bench.py --no-cpu --no-host --no-sizes --no-configs --steps 5 --warmup 1 || exit $? ;;
     pmcab)  # decode vs encode, occupancy-capped (a) vs uncapped (u): HBM request queue depth and stalls
         PA="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_LEVEL_sum GRBM_GUI_ACTIVE"
         PB="TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum TCC_TOO_MANY_EA_WRREQS_STALL_sum GRBM_GUI_ACTIVE"
@@ -41,7 +41,7 @@ for step in "$@"; do
             lib=""; [ $v = a ] || lib="$PWD/elect_amd/_ab/libelect_ec_$v.so"
             ctr=$PA; [ $pass = B ] && ctr=$PB
             ELECT_EC_LIB=$lib run pmcab_${v}_$pass 120 rocprofv3 --pmc $ctr --output-format csv -d $OUT/pmcab_${v}_$pass -o run \
-                -- python3 bench.py --no-cpu --no-host --no-sizes --steps 5 --warmup 1 || exit $?
+                -- python3 bench.py --no-cpu --no-host --no-sizes --no-configs --steps 5 --warmup 1 || exit $?
         done; done ;;
     profcfg)  # rocprof kernel stats of one bench config: PROF_CFG="--config hashed ..."
         run profcfg 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profcfg_$TAG -o run \
@@ -76,8 +76,8 @@ for step in "$@"; do
         run bench_rehearse_8rank 600 python bench.py --gpus 8 --steps 10 --warmup 2 --no-cpu --no-host --rotate 2 || exit $?
         unset ELECT_BENCH_SHARE_GPU ;;
     graph)  # host submit time: eager vs HIP-graph replay, headline and mixed
-        run bench_eager_nosizes 300 python bench.py --no-cpu --no-host --no-sizes --steps 50 || exit $?
-        run bench_graph 300 python bench.py --graph --no-cpu --no-host --no-sizes --steps 50 || exit $?
+        run bench_eager_nosizes 300 python bench.py --no-cpu --no-host --no-sizes --no-configs --steps 50 || exit $?
+        run bench_graph 300 python bench.py --graph --no-cpu --no-host --no-sizes --no-configs --steps 50 || exit $?
         run bench_mixed_eager 300 python bench.py --config mixed --steps 20 || exit $?
         run bench_mixed_graph 300 python bench.py --config mixed --graph --steps 20 || exit $? ;;
     mixedshare)  # the mixed config's per-GPU share at 2/4/8 GPUs, eager and graph-replayed
