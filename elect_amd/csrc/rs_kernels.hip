@@ -164,19 +164,25 @@ __device__ __forceinline__ uint32_t dpow31(uint64_t e)
 
 // sum_t sb[t] * 31^t over the 16 bytes of a segment.  v_dot4_i32_i8 reads the
 // bytes as signed int8, which is Java's byte: per dword D = (b0 + 31 b1) +
-// 961 (b2 + 31 b3), then a Horner step of 31^4 per dword.
+// 961 (b2 + 31 b3), |D| < 2^22.  Then D0 + 31^4 D1 and D2 + 31^4 D3 as 24-bit
+// multiplies (full rate; the low 32 bits are exact mod 2^32), and one 32-bit
+// multiply by 31^8 (v_mul_lo_u32 is quarter rate: one instead of a three-step
+// Horner chain).
 __device__ __forceinline__ uint32_t horner31(const uint4& v)
 {
-    uint32_t h = 0;
+    int d[4];
 #pragma unroll
-    for (int w = 3; w >= 0; --w) {
+    for (int w = 0; w < 4; ++w) {
         const int x = static_cast<int>(lane_word(v, w));
         const int lo = __builtin_amdgcn_sdot4(x, 0x00001F01, 0, false);
         const int hi = __builtin_amdgcn_sdot4(x, 0x1F010000, 0, false);
-        const uint32_t d = static_cast<uint32_t>(__mul24(hi, 961) + lo);
-        h = w == 3 ? d : h * 923521u + d;  // 923521 = 31^4
+        d[w] = __mul24(hi, 961) + lo;
     }
-    return h;
+    constexpr uint32_t kP4 = 923521u;  // 31^4 (< 2^23)
+    constexpr uint32_t kP8 = kP4 * kP4;  // 31^8 mod 2^32
+    const uint32_t t01 = static_cast<uint32_t>(__mul24(d[1], static_cast<int>(kP4)) + d[0]);
+    const uint32_t t23 = static_cast<uint32_t>(__mul24(d[3], static_cast<int>(kP4)) + d[2]);
+    return t23 * kP8 + t01;
 }
 
 // 31^(16*seg) for a 32-bit segment index seg, from four 256-entry tables
@@ -567,7 +573,29 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 // masked, so no byte loads.  Straddling waves take a one-segment-at-a-time path.
 constexpr int kAuxNT = 2;  // buffer op cache policy: nt (gfx940 family CPol)
 
-template <int K, int R, int U>
+// HASH (add mode only: entries seeded with 31^len by launch_apply): a wave
+// inside one stripe sums its U*64 segments' hash terms in registers (constant
+// 31^(1024u) weights per slice) and writes ONE partial per row, into the slot
+// of its first 64-segment group, zeros into its other U-1 slots (hash_reduce
+// adds the slots of every group wholly inside a stripe); a straddling wave
+// zeroes its slots and adds per lane atomically.  So the wave reduction is paid
+// once per U KiB per column instead of once per KiB (gf_apply_x16<.., HASH>).
+template <int U>
+struct SlicePow {  // 31^(16*64*u), u < U
+    uint32_t v[U];
+    constexpr SlicePow() : v()
+    {
+        uint32_t p = 1;
+        for (int i = 0; i < 1024; ++i) p *= 31u;
+        uint32_t x = 1;
+        for (int u = 0; u < U; ++u) {
+            v[u] = x;
+            x *= p;
+        }
+    }
+};
+
+template <int K, int R, int U, bool HASH>
 __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
@@ -613,6 +641,9 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
                 if (off0 < sl[j] && sl[j] < off0 + 1024u && (sl[j] & 15u))  // wave-uniform: this slice holds the content end
                     x[u][j] = keep_bytes(x[u][j], off < sl[j] ? min(sl[j] - off, 16u) : 0u);
         }
+        uint32_t hacc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) hacc[r] = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t idx = first + u * 64u + lane;
@@ -629,8 +660,39 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
             gf_combine<K, R, true>(x[u], tl, acc, cmask);
 #pragma unroll
             for (int r = 0; r < R; ++r) store_nt(a.dp[r] + s0 * a.ds[r] + off, acc[r]);
+            if constexpr (HASH) {
+                constexpr SlicePow<U> kSlice{};
+#pragma unroll
+                for (int r = 0; r < R; ++r) hacc[r] += u == 0 ? horner31(acc[r]) : horner31(acc[r]) * kSlice.v[u];
+            }
+        }
+        if constexpr (HASH) {
+            if (a.hashes) {  // the whole wave again (the slice loop may have left early)
+                const uint32_t hs = div_magic(first, a.hmagic, a.hshift);
+                const uint32_t q = kLanePow.v[lane] * (a.hpow * pow31_seg(first - hs * a.hsegs));
+                const uint64_t slot = first >> 6;
+                // hash_reduce reads only 64-segment groups wholly inside the launch: a
+                // wave reaching its end adds per lane instead (lanes past it hold 0)
+                const bool tail = first + 64u * U > a.total;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (tail) {
+                        if (hacc[r]) atomicAdd(reinterpret_cast<unsigned*>(a.hashes) + static_cast<uint64_t>(hs) * a.hstride + r,
+                                               hacc[r] * q);
+                        if (lane < U && first + 64u * lane < a.total) a.hpart[(slot + lane) * R + r] = 0u;
+                        continue;
+                    }
+                    const uint32_t sum = wave_sum(hacc[r] * q);
+                    if (lane < U) a.hpart[(slot + lane) * R + r] = lane == 0 ? sum : 0u;
+                }
+            }
         }
         return;
+    }
+    if (HASH && a.hashes) {  // straddling wave: its slots read as zero, terms added per lane below
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (lane < U && first + 64u * lane < a.total) a.hpart[((first >> 6) + lane) * R + r] = 0u;
     }
     for (int u = 0; u < U; ++u) {  // straddling wave: per-lane stripes and lengths
         const uint32_t idx = first + u * 64u + lane;
@@ -652,6 +714,14 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
         gf_combine<K, R>(x, tl, acc);
 #pragma unroll
         for (int r = 0; r < R; ++r) store_nt(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
+        if (HASH && a.hashes) {
+            const uint32_t hs = div_magic(idx, a.hmagic, a.hshift);
+            const uint32_t p = a.hpow * pow31_seg(idx - hs * a.hsegs);
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                atomicAdd(reinterpret_cast<unsigned*>(a.hashes) + static_cast<uint64_t>(hs) * a.hstride + r,
+                          horner31(acc[r]) * p);
+        }
     }
 }
 
@@ -895,6 +965,30 @@ hipError_t scratch_release(ScratchEntry* e, hipStream_t stream)
     return err;
 }
 
+// Padded launches the per-stripe-length kernel can take (whole 16-byte segments,
+// aligned columns).  Hashed ones with per-stripe content lengths, untiled, of at
+// most 4 columns take it too, 2 segments per lane, in add mode only (launch_apply_impl
+// seeds the entries for them).  Interleaved A/B against gf_apply_x16<.., HASH>
+// (profiles/r02_lenshash_ab/): ELECT's fused steps at 64 KiB codeLength, encode
+// 73.1 -> 74.2 %, update 74.6 -> 76.0 %; but ELECT's 4.4 MB codeLength in tiles lost
+// 2 points (79.5 -> 77.6 %), full hashed units 1 % (3,762 -> 3,725 GiB/s), and
+// 4 segments per lane (121 VGPRs) or 1 lost everywhere: those stay on gf_apply_x16.
+#ifndef AB_LENS_HASH
+#define AB_LENS_HASH 1
+#endif
+#ifndef AB_LENS_HASH_U
+#define AB_LENS_HASH_U 2
+#endif
+inline bool lens_eligible(const ApplyParams& p)
+{
+    return p.aligned16 && p.len % 16 == 0 && p.len > 0 && p.len < (uint64_t{1} << 31);
+}
+
+inline bool lens_hash_path(const ApplyParams& p)
+{
+    return AB_LENS_HASH && p.hashes && p.padded && p.lens && p.tiles <= 1 && p.cols <= 4 && lens_eligible(p);
+}
+
 template <int K, int R, bool PAD>
 hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
 {
@@ -955,16 +1049,23 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         }
         bool lens_path = false;
         if constexpr (PAD) {
-            lens_path = (a.lens || tiles > 1) && !a.hashes && p.aligned16 && p.len % 16 == 0 &&
-                        p.len < (uint64_t{1} << 31);
+            lens_path = a.hashes ? lens_hash_path(p) && !hash_assign : (a.lens || tiles > 1) && lens_eligible(p);
 #ifdef AB_NO_LENS
             lens_path = false;
 #endif
             if (lens_path) {
                 constexpr int U = lens_unroll<K>();
                 const uint64_t threads = (static_cast<uint64_t>(a.total) + 64 * U - 1) / (64 * U) * 64;
-                hipLaunchKernelGGL((gf_apply_lens<K, R, U>), dim3(static_cast<uint32_t>((threads + block - 1) / block)),
-                                   dim3(block), lens_cap(block, R * K, K, R), stream, a);
+                const dim3 grid(static_cast<uint32_t>((threads + block - 1) / block));
+                if (!a.hashes)
+                    hipLaunchKernelGGL((gf_apply_lens<K, R, U, false>), grid, dim3(block), lens_cap(block, R * K, K, R),
+                                       stream, a);
+                else if constexpr (K <= 4) {  // (lens_hash_path)
+                    constexpr int UH = AB_LENS_HASH_U;
+                    const uint64_t th = (static_cast<uint64_t>(a.total) + 64 * UH - 1) / (64 * UH) * 64;
+                    hipLaunchKernelGGL((gf_apply_lens<K, R, UH, true>), dim3(static_cast<uint32_t>((th + block - 1) / block)),
+                                       dim3(block), 0, stream, a);
+                }
             }
         }
         if (!lens_path) {
@@ -1386,11 +1487,11 @@ hipError_t launch_apply_impl(const ApplyParams& p_in, hipStream_t stream)
                       !vec || p.cols > kMaxPadCols || wide_hash))
         return hipErrorInvalidValue;  // tiling rides on the padded vector kernels only
     if (p.hashes && p.hash_seed) {
-        // Assign mode needs the fast kernel with >= 64 segments per hashed unit
-        // (every wave within two units); anything else seeds the entries and adds.
+        // Assign mode needs the one-segment fast kernel with >= 64 segments per hashed
+        // unit (every wave within two units); anything else seeds the entries and adds.
         const bool fast = vec && (!p.padded || p.cols <= kMaxPadCols) && !wide_hash;
         const uint64_t segs = (p.padded ? (p.len + 15) / 16 : p.len / 16) * tiles;
-        if (!fast || segs < 64) {
+        if (!fast || segs < 64 || lens_hash_path(p)) {
             const hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.hashes), static_cast<int>(pow31(ulen)),
                                                    p.stripes / tiles * p.hash_stride, stream);
             if (e != hipSuccess) return e;
