@@ -63,6 +63,7 @@ for step in "$@"; do
           ls /usr/lib/x86_64-linux-gnu /usr/local/lib /opt/rocm/lib 2>/dev/null | grep -i isal || echo "no libisal files"; } \
             > gpurun_out/envprobe.log 2>&1; cat gpurun_out/envprobe.log ;;
     probe) run probe 300 tools/tune/tune_apply probe || exit $? ;;
+    policy) run policy 300 tools/tune/tune_apply policy && TUNE_ROTATE=4 run policy_rot4 300 tools/tune/tune_apply policy || exit $? ;;  # buffer-op cache-policy bits, 4-in/1-2-out streams
     streams) run streams 300 tools/tune/tune_apply streams || exit $? ;;
     unitstride) run unitstride 300 tools/tune/tune_apply unitstride || exit $? ;;
     unaligned) run unaligned 120 tools/tune/tune_apply unaligned || exit $? ;;

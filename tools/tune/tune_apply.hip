@@ -646,6 +646,79 @@ static void stream_probe()
     CK(hipFree(sink));
 }
 
+// Cache-policy probe: the decode (4 in, 1 out) and encode (4 in, 2 out) access
+// patterns of the [B][6][L] layout through buffer loads/stores with explicit
+// gfx940-family CPol bits (aux: sc0 = 1, nt = 2, sc1 = 16), to see whether any
+// policy other than the product's nt/nt streams HBM better.
+template <int W, int LA, int SA>
+__global__ void policy_kernel(const uint8_t* in, uint8_t* out, uint32_t* sink, uint32_t L, uint32_t segs,
+                              uint32_t total)
+{
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const uint32_t st = idx / segs;
+    const uint32_t off = (idx - st * segs) * 16;
+    const __amdgpu_buffer_rsrc_t ri =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(in + static_cast<uint64_t>(st) * 6 * L), 0, 6 * L, 0x00020000);
+    uint32_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(ri, static_cast<int>(off + s * L), 0, LA);
+        v0 ^= x[0]; v1 ^= x[1]; v2 ^= x[2]; v3 ^= x[3];
+    }
+    const __amdgpu_buffer_rsrc_t ro =
+        __builtin_amdgcn_make_buffer_rsrc(out + static_cast<uint64_t>(st) * W * L, 0, W * L, 0x00020000);
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        const v4u y = {v0 + w, v1, v2, v3};
+        __builtin_amdgcn_raw_buffer_store_b128(y, ro, static_cast<int>(off + w * L), 0, SA);
+    }
+}
+
+static void policy_probe()
+{
+    // TUNE_ROTATE=N: launches cycle over N disjoint input/output sets, so no launch
+    // finds the previous one's output lines (dirty) in L2 or the 256 MiB MALL
+    const int nrot = std::getenv("TUNE_ROTATE") ? std::max(1, std::atoi(std::getenv("TUNE_ROTATE"))) : 1;
+    const uint32_t L = 65536, B = 4096;
+    const uint32_t segs = L / 16, total = B * segs;
+    uint8_t *a0, *b0;
+    uint32_t* sink;
+    CK(hipMalloc(&a0, static_cast<uint64_t>(B) * 6 * L * nrot));
+    CK(hipMalloc(&b0, static_cast<uint64_t>(B) * 2 * L * nrot));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMemset(a0, 7, static_cast<uint64_t>(B) * 6 * L * nrot));
+    int turn = 0;
+    uint8_t *a = a0, *b = b0;
+    auto next = [&] {
+        const int i = turn++ % nrot;
+        a = a0 + static_cast<uint64_t>(B) * 6 * L * i;
+        b = b0 + static_cast<uint64_t>(B) * 2 * L * i;
+    };
+    std::printf("policy probe: %d rotating sets\n", nrot);
+    const dim3 g((total + 255) / 256);
+    const double seg = 16.0 * total;
+    auto rep = [&](const char* name, double moved, float ms) {
+        std::printf("policy %-34s %8.4f ms  %7.1f GB/s  %5.1f%% of 8 TB/s\n", name, ms, moved / (ms * 1e-3) / 1e9,
+                    100.0 * moved / (ms * 1e-3) / 8e12);
+    };
+    for (int round = 0; round < 3; ++round) {
+#define PP(W, LA, SA) rep(#W " out ld=" #LA " st=" #SA, seg * (4 + W), median_ms([&] { next(); \
+        hipLaunchKernelGGL((policy_kernel<W, LA, SA>), g, dim3(256), 0, 0, a, b, sink, L, segs, total); }))
+        rep("1 out global nt/nt (product)", seg * 5, median_ms([&] { next();
+            hipLaunchKernelGGL((stream_kernel<4, 1, true>), g, dim3(256), 0, 0, a, b, sink, uint64_t{L}, segs, total); }));
+        PP(1, 2, 2); PP(1, 18, 2); PP(1, 2, 0); PP(1, 2, 16); PP(1, 2, 1); PP(1, 18, 16);
+        rep("2 out global nt/nt (product)", seg * 6, median_ms([&] { next();
+            hipLaunchKernelGGL((stream_kernel<4, 2, true>), g, dim3(256), 0, 0, a, b, sink, uint64_t{L}, segs, total); }));
+        PP(2, 2, 2); PP(2, 18, 2); PP(2, 2, 0); PP(2, 2, 16); PP(2, 2, 1); PP(2, 18, 16);
+#undef PP
+    }
+    CK(hipFree(a0));
+    CK(hipFree(b0));
+    CK(hipFree(sink));
+}
+
 // Encode-shaped XOR probe with a runtime unit stride U: stripe s's unit j at
 // s*6*U + j*U, L <= U bytes used per unit; units 0..3 read, 4..5 written in
 // place.  Asks whether the 64 KiB sweet spot is about the unit
@@ -770,6 +843,10 @@ int main(int argc, char** argv)
     }
     if (argc > 1 && std::string(argv[1]) == "unitstride") {
         unit_stride_probe();
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "policy") {
+        policy_probe();
         return 0;
     }
     if (argc > 1 && std::string(argv[1]) == "probe") {
