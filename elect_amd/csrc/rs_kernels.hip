@@ -537,7 +537,17 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
             const uint32_t q = kLanePow.v[threadIdx.x & 63u] * p0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
+#if defined(AB_HASH_NOSUM)  // timing probes only (wrong hashes): no wave reduction / no Horner
+                const uint32_t sum = horner31(acc[r]) * q;
+#elif defined(AB_HASH_NOHORNER)
+                const uint32_t sum = wave_sum(acc[r].x * q);
+#elif defined(AB_HASH_ROWSUM)  // row sums only (4 DPP steps, no row broadcasts)
+                uint32_t v = horner31(acc[r]) * q;
+                v = dpp_add<0xB1>(v); v = dpp_add<0x4E>(v); v = dpp_add<0x124>(v); v = dpp_add<0x128>(v);
+                const uint32_t sum = v;
+#else
                 const uint32_t sum = wave_sum(horner31(acc[r]) * q);
+#endif
                 if ((threadIdx.x & 63u) == 0) a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum;
             }
         } else if (a.hpart_hi) {  // assign mode: a wave straddling two stripes (or the launch's end)
