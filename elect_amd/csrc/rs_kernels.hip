@@ -573,6 +573,30 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
     }
 }
 
+// Plain launches whose stripes hold whole waves (segs % 64 == 0, offsets inside a
+// stripe below 2^32): every wave lies in one stripe, so its column addresses
+// are scalar bases (stripe * stride in SALU) plus one 32-bit lane offset, not a
+// 64-bit multiply-add per column and lane (v_mad_u64_u32: 27 per lane in
+// RS(12,8) encode, 15 in RS(6,4) encode).
+template <int K, int R>
+__global__ __launch_bounds__(kBlock) void gf_apply_x16u(const FastArgs<K, R> a)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t first = __builtin_amdgcn_readfirstlane(idx);  // the wave's lane 0
+    const uint32_t stripe = div_magic(first, a.magic, a.shift);  // wave-uniform
+    const uint32_t off = (idx - stripe * a.segs) * 16u;
+    stage_tables<K, R>(a.tab, tl);
+    if (first >= a.total) return;  // total % 64 == 0: waves are wholly live or wholly past the end
+    uint4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + static_cast<uint64_t>(stripe) * a.ss[j] + off);
+    uint4 acc[R];
+    gf_combine<K, R>(x, tl, acc);
+#pragma unroll
+    for (int r = 0; r < R; ++r) store_nt(a.dp[r] + static_cast<uint64_t>(stripe) * a.ds[r] + off, acc[r]);
+}
+
 // Padded launches with per-stripe content lengths, no hash, and L % 16 == 0:
 // U segments per lane.  The lengths sit on the critical path of every data
 // load (no load past a unit's content), so a wave amortises that dependent
@@ -762,7 +786,9 @@ struct GroupArgs {
     gf::PermTable tab[R][K];
 };
 
-template <int K, int R>
+// UNI: every part's stripes hold whole waves (segs % 64 == 0, stripe offsets
+// below 2^32): scalar stripe bases, as gf_apply_x16u.
+template <int K, int R, bool UNI>
 __global__ __launch_bounds__(kBlock) void gf_apply_group(const GroupArgs<K, R> a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
@@ -772,9 +798,11 @@ __global__ __launch_bounds__(kBlock) void gf_apply_group(const GroupArgs<K, R> a
     const GroupPart<K, R>& g = a.part[p];
     const uint32_t idx = (blockIdx.x - g.block0) * blockDim.x + threadIdx.x;
     stage_tables<K, R>(a.tab, tl);
-    if (idx >= g.total) return;
-    const uint32_t stripe = static_cast<uint32_t>((static_cast<uint64_t>(idx) * g.magic) >> g.shift);
-    const uint64_t off = static_cast<uint64_t>(idx - stripe * g.segs) * 16;
+    if (idx >= g.total) return;  // (UNI: whole waves)
+    const uint32_t stripe = UNI ? div_magic(__builtin_amdgcn_readfirstlane(idx), g.magic, g.shift)
+                                : static_cast<uint32_t>((static_cast<uint64_t>(idx) * g.magic) >> g.shift);
+    const uint64_t off = UNI ? static_cast<uint64_t>(static_cast<uint32_t>((idx - stripe * g.segs) * 16u))
+                             : static_cast<uint64_t>(idx - stripe * g.segs) * 16;
     uint4 x[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) x[j] = load_nt(g.sp[j] + stripe * g.ss[j] + off);
@@ -999,6 +1027,16 @@ inline bool lens_hash_path(const ApplyParams& p)
     return AB_LENS_HASH && p.hashes && p.padded && p.lens && p.tiles <= 1 && p.cols <= 4 && lens_eligible(p);
 }
 
+// gf_apply_x16u (and the grouped kernel's UNI form) for plain launches of
+// whole-wave stripes with at least this many columns.  Interleaved A/B
+// (profiles/r02_scalarbase_ab/): RS(12,8) two-erasure decode (K = 8) 79.9 ->
+// 81.6 % of peak, 4,618 -> 4,716 GiB/s; RS(6,4) encode 82.7 -> 82.2 %, its
+// decode +0.5, the mixed config -0.5 %: the four-column shapes keep the
+// per-lane addressing.  AB builds: -DAB_SCALAR_BASE_MIN_K=99 turns it off.
+#ifndef AB_SCALAR_BASE_MIN_K
+#define AB_SCALAR_BASE_MIN_K 8
+#endif
+
 template <int K, int R, bool PAD>
 hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
 {
@@ -1080,7 +1118,14 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         }
         if (!lens_path) {
             const uint32_t grid = (a.total + block - 1) / block;
-            if (!a.hashes) {
+            bool scalar_base = false;
+            if constexpr (!PAD && K >= AB_SCALAR_BASE_MIN_K)
+                scalar_base = !a.hashes && a.segs % 64 == 0 && segs64 < (uint64_t{1} << 28);
+            if (scalar_base) {
+                if constexpr (!PAD && K >= AB_SCALAR_BASE_MIN_K)
+                    hipLaunchKernelGGL((gf_apply_x16u<K, R>), dim3(grid), dim3(block),
+                                       cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
+            } else if (!a.hashes) {
                 hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, false>), dim3(grid), dim3(block),
                                    PAD ? 0 : cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
             } else if constexpr (K <= kMaxHashCols) {
@@ -1147,7 +1192,11 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
     for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(ps[0].coef[(r0 + r) * ps[0].cols + j]);
     int block = kBlock;
-    for (int i = 0; i < n; ++i) block = std::min(block, block_for(ps[i].len, R * K));
+    bool uni = true;  // (used for K >= AB_SCALAR_BASE_MIN_K)
+    for (int i = 0; i < n; ++i) {
+        block = std::min(block, block_for(ps[i].len, R * K));
+        uni = uni && (ps[i].len / 16) % 64 == 0 && ps[i].len < (uint64_t{1} << 32);
+    }
     if (AB_GROUP_BLOCK > 0) block = AB_GROUP_BLOCK;
     uint64_t blocks = 0;
     for (int i = 0; i < n; ++i) {
@@ -1171,7 +1220,14 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
         blocks += (g.total + block - 1) / block;
     }
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((gf_apply_group<K, R>), dim3(static_cast<uint32_t>(blocks)), dim3(block),
+    if constexpr (K >= AB_SCALAR_BASE_MIN_K) {
+        if (uni) {
+            hipLaunchKernelGGL((gf_apply_group<K, R, true>), dim3(static_cast<uint32_t>(blocks)), dim3(block),
+                               cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((gf_apply_group<K, R, false>), dim3(static_cast<uint32_t>(blocks)), dim3(block),
                        cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
     return hipGetLastError();
 }
