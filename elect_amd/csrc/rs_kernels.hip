@@ -578,7 +578,9 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 // are scalar bases (stripe * stride in SALU) plus one 32-bit lane offset, not a
 // 64-bit multiply-add per column and lane (v_mad_u64_u32: 27 per lane in
 // RS(12,8) encode, 15 in RS(6,4) encode).
-template <int K, int R>
+// HASH: every wave lies inside one hashed unit, so it writes one partial per
+// row (hash_reduce reads it in either mode: no wave starts outside its unit).
+template <int K, int R, bool HASH>
 __global__ __launch_bounds__(kBlock) void gf_apply_x16u(const FastArgs<K, R> a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
@@ -595,6 +597,17 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16u(const FastArgs<K, R> a)
     gf_combine<K, R>(x, tl, acc);
 #pragma unroll
     for (int r = 0; r < R; ++r) store_nt(a.dp[r] + static_cast<uint64_t>(stripe) * a.ds[r] + off, acc[r]);
+    if constexpr (HASH) {
+        if (a.hashes) {
+            const uint32_t hs = div_magic(first, a.hmagic, a.hshift);
+            const uint32_t q = kLanePow.v[threadIdx.x & 63u] * (a.hpow * pow31_seg(first - hs * a.hsegs));
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t sum = wave_sum(horner31(acc[r]) * q);
+                if ((threadIdx.x & 63u) == 0) a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum;
+            }
+        }
+    }
 }
 
 // Padded launches with per-stripe content lengths, no hash, and L % 16 == 0:
@@ -1036,6 +1049,9 @@ inline bool lens_hash_path(const ApplyParams& p)
 #ifndef AB_SCALAR_BASE_MIN_K
 #define AB_SCALAR_BASE_MIN_K 8
 #endif
+#ifndef AB_SCALAR_BASE_HASH  // hashed plain launches of whole-wave stripes, any width
+#define AB_SCALAR_BASE_HASH 1
+#endif
 
 template <int K, int R, bool PAD>
 hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
@@ -1119,12 +1135,19 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         if (!lens_path) {
             const uint32_t grid = (a.total + block - 1) / block;
             bool scalar_base = false;
-            if constexpr (!PAD && K >= AB_SCALAR_BASE_MIN_K)
-                scalar_base = !a.hashes && a.segs % 64 == 0 && segs64 < (uint64_t{1} << 28);
+            if constexpr (!PAD)
+                scalar_base = (a.hashes ? AB_SCALAR_BASE_HASH != 0 && K <= kMaxHashCols : K >= AB_SCALAR_BASE_MIN_K) &&
+                              a.segs % 64 == 0 && segs64 < (uint64_t{1} << 28);
             if (scalar_base) {
-                if constexpr (!PAD && K >= AB_SCALAR_BASE_MIN_K)
-                    hipLaunchKernelGGL((gf_apply_x16u<K, R>), dim3(grid), dim3(block),
-                                       cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
+                if constexpr (!PAD && K >= AB_SCALAR_BASE_MIN_K) {
+                    if (!a.hashes)
+                        hipLaunchKernelGGL((gf_apply_x16u<K, R, false>), dim3(grid), dim3(block),
+                                           cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
+                }
+                if constexpr (!PAD && K <= kMaxHashCols) {
+                    if (a.hashes)
+                        hipLaunchKernelGGL((gf_apply_x16u<K, R, true>), dim3(grid), dim3(block), 0, stream, a);
+                }
             } else if (!a.hashes) {
                 hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, false>), dim3(grid), dim3(block),
                                    PAD ? 0 : cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
