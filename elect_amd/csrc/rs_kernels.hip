@@ -1049,6 +1049,9 @@ inline bool lens_hash_path(const ApplyParams& p)
 #ifndef AB_SCALAR_BASE_MIN_K
 #define AB_SCALAR_BASE_MIN_K 8
 #endif
+#ifndef AB_SCALAR_BASE_R1  // A/B: single-row plain launches (one-erasure decodes) of any width too
+#define AB_SCALAR_BASE_R1 0
+#endif
 #ifndef AB_SCALAR_BASE_HASH  // hashed plain launches of whole-wave stripes, any width
 #define AB_SCALAR_BASE_HASH 1
 #endif
@@ -1135,11 +1138,12 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         if (!lens_path) {
             const uint32_t grid = (a.total + block - 1) / block;
             bool scalar_base = false;
+            constexpr bool kPlainU = K >= AB_SCALAR_BASE_MIN_K || (AB_SCALAR_BASE_R1 && R == 1);
             if constexpr (!PAD)
-                scalar_base = (a.hashes ? AB_SCALAR_BASE_HASH != 0 && K <= kMaxHashCols : K >= AB_SCALAR_BASE_MIN_K) &&
+                scalar_base = (a.hashes ? AB_SCALAR_BASE_HASH != 0 && K <= kMaxHashCols : kPlainU) &&
                               a.segs % 64 == 0 && segs64 < (uint64_t{1} << 28);
             if (scalar_base) {
-                if constexpr (!PAD && K >= AB_SCALAR_BASE_MIN_K) {
+                if constexpr (!PAD && kPlainU) {
                     if (!a.hashes)
                         hipLaunchKernelGGL((gf_apply_x16u<K, R, false>), dim3(grid), dim3(block),
                                            cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
