@@ -297,6 +297,7 @@ def decode_sweep(coder, stripe, k, m, L, B, stream, reps=5):
     """Single-erasure decode for each data shard j (survivors: the other k of
     shards 0..k), outside the timed region: per-kernel GB/s and HBM fraction."""
     from elect_amd.batch import decode_batch
+    B, L = stripe.shape[0], stripe.shape[2]  # the coding view (tiled layouts: B*T stripes of 64 KiB)
     out = torch.empty((B, 1, L), dtype=torch.uint8, device=stripe.device)
     res = {}
     for j in range(k):

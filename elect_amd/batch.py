@@ -29,6 +29,24 @@ def _column(t: torch.Tensor) -> ColumnT:
     return ColumnT(t.data_ptr(), t.stride(0))
 
 
+def _rows(name: str, t: torch.Tensor, B: int, L: int, need: int) -> None:
+    """t must be [B, >= need, L]: the C ABI addresses it from its strides alone, so a
+    tensor of another shape would be read or written out of bounds on the device."""
+    if t.dim() != 3 or t.shape[0] != B or t.shape[2] != L or t.shape[1] < need:
+        raise ValueError(f"{name}: expected [{B}, >={need}, {L}], got {tuple(t.shape)}")
+
+
+def _decode_shapes(coder, inputs, decode_indexes, erased, outputs, inputs_by_unit, outputs_by_unit):
+    if len(decode_indexes) != coder.k:
+        raise ValueError("decode_indexes needs exactly k entries")
+    if inputs.dim() != 3:
+        raise ValueError(f"inputs: expected a [stripes, units, L] tensor, got {tuple(inputs.shape)}")
+    B, _, L = inputs.shape
+    _rows("inputs", inputs, B, L, max(decode_indexes) + 1 if inputs_by_unit else coder.k)
+    _rows("outputs", outputs, B, L, max(erased) + 1 if outputs_by_unit and len(erased) else len(erased))
+    return B, L
+
+
 def _stream(stream) -> int:
     if stream is None:
         stream = torch.cuda.current_stream()
@@ -75,10 +93,8 @@ def decode_batch(coder: RSCoder, inputs: torch.Tensor, decode_indexes, erased, o
     inputs: [B, k, L] survivors in decode_indexes order, or (inputs_by_unit)
     a [B, k+m, L] stripe tensor read at rows decode_indexes.  outputs: [B, e, L],
     or (outputs_by_unit) the stripe tensor, written at rows erased."""
-    B, _, L = inputs.shape
+    B, L = _decode_shapes(coder, inputs, decode_indexes, erased, outputs, inputs_by_unit, outputs_by_unit)
     flags = (_lib.INPUTS_BY_UNIT if inputs_by_unit else 0) | (_lib.OUTPUTS_BY_UNIT if outputs_by_unit else 0)
-    if len(decode_indexes) != coder.k:
-        raise ValueError("decode_indexes needs exactly k entries")
     return check(lib.elect_ec_decode_batch(coder.handle, L, B, _shards(inputs), int_array(decode_indexes),
                                            int_array(erased), len(erased), _shards(outputs), flags, mode,
                                            _stream(stream)), "decode_batch")
@@ -89,10 +105,8 @@ def decode_batch_ex(coder: RSCoder, inputs: torch.Tensor, decode_indexes, erased
                     outputs_by_unit: bool = False, stream=None) -> int:
     """decode_batch over zero-padded survivors (ECRecovery.java:128-141): lengths[s, j] content
     bytes of survivor j (decode_indexes order; int32 device tensor [B, k], each <= L)."""
-    B, _, L = inputs.shape
+    B, L = _decode_shapes(coder, inputs, decode_indexes, erased, outputs, inputs_by_unit, outputs_by_unit)
     flags = (_lib.INPUTS_BY_UNIT if inputs_by_unit else 0) | (_lib.OUTPUTS_BY_UNIT if outputs_by_unit else 0)
-    if len(decode_indexes) != coder.k:
-        raise ValueError("decode_indexes needs exactly k entries")
     return check(lib.elect_ec_decode_batch_ex(coder.handle, L, B, _shards(inputs),
                                               _lengths(lengths, B, coder.k, inputs.device),
                                               int_array(decode_indexes), int_array(erased), len(erased),
@@ -102,10 +116,19 @@ def decode_batch_ex(coder: RSCoder, inputs: torch.Tensor, decode_indexes, erased
 def encode_update_batch(coder: RSCoder, target: int, old: torch.Tensor, new: torch.Tensor,
                         parity_in: torch.Tensor, parity_out: torch.Tensor, stream=None) -> None:
     """parity_out[s, r] = parity_in[s, r] ^ E[k+r][target] * (old[s] ^ new[s]); in place allowed."""
-    B, L = old.shape
+    B, L = _update_shapes(coder, old, new, parity_in, parity_out)
     check(lib.elect_ec_encode_update_batch(coder.handle, L, B, target, _column(old), _column(new),
                                            _shards(parity_in), _shards(parity_out), _stream(stream)),
           "encode_update_batch")
+
+
+def _update_shapes(coder, old, new, parity_in, parity_out):
+    if old.dim() != 2 or new.shape != old.shape:
+        raise ValueError(f"old/new: expected two [stripes, L] tensors, got {tuple(old.shape)} {tuple(new.shape)}")
+    B, L = old.shape
+    _rows("parity_in", parity_in, B, L, coder.m)
+    _rows("parity_out", parity_out, B, L, coder.m)
+    return B, L
 
 
 def _lengths(lengths, B: int, n: int, device) -> int:
@@ -145,7 +168,7 @@ def encode_update_batch_ex(coder: RSCoder, target: int, old: torch.Tensor, new: 
     """ELECT's parity-update step in one launch (ECParityUpdateVerbHandler.java:634-699):
     old[s] / new[s] hold lengths[s, 0] / lengths[s, 1] content bytes (None: full), the
     new parity goes to parity_out (may be parity_in) and its hashCode() to hashes[s, r]."""
-    B, L = old.shape
+    B, L = _update_shapes(coder, old, new, parity_in, parity_out)
     check(lib.elect_ec_encode_update_batch_ex(coder.handle, L, B, target, _column(old), _column(new),
                                               _lengths(lengths, B, 2, old.device), _shards(parity_in),
                                               _shards(parity_out), _hashes(hashes, B, coder.m, old.device),
@@ -180,7 +203,7 @@ def encode_update_batch_tiled(coder: RSCoder, target: int, old: torch.Tensor, ne
                               parity_in: torch.Tensor, parity_out: torch.Tensor, chunk_size: int, lengths=None,
                               hashes=None, stream=None) -> None:
     """encode_update_batch_ex over tiled units: old/new [B*T, tile], parity [B*T, m, tile]."""
-    rows, tile = old.shape
+    rows, tile = _update_shapes(coder, old, new, parity_in, parity_out)
     B = _tiles_of(chunk_size, tile, rows)
     check(lib.elect_ec_encode_update_batch_tiled(coder.handle, chunk_size, tile, B, target, _column(old), _column(new),
                                                  _lengths(lengths, B, 2, old.device), _shards(parity_in),
@@ -193,11 +216,9 @@ def decode_batch_tiled(coder: RSCoder, inputs: torch.Tensor, decode_indexes, era
                        chunk_size: int, lengths=None, mode: int = _lib.DECODE_COMPAT, inputs_by_unit: bool = False,
                        outputs_by_unit: bool = False, stream=None) -> int:
     """decode_batch_ex over tiled units: inputs [B*T, k or k+m, tile], outputs [B*T, e or k+m, tile]."""
-    rows, _, tile = inputs.shape
+    rows, tile = _decode_shapes(coder, inputs, decode_indexes, erased, outputs, inputs_by_unit, outputs_by_unit)
     B = _tiles_of(chunk_size, tile, rows)
     flags = (_lib.INPUTS_BY_UNIT if inputs_by_unit else 0) | (_lib.OUTPUTS_BY_UNIT if outputs_by_unit else 0)
-    if len(decode_indexes) != coder.k:
-        raise ValueError("decode_indexes needs exactly k entries")
     return check(lib.elect_ec_decode_batch_tiled(coder.handle, chunk_size, tile, B, _shards(inputs),
                                                  _lengths(lengths, B, coder.k, inputs.device),
                                                  int_array(decode_indexes), int_array(erased), len(erased),
@@ -224,7 +245,7 @@ def decode_batches(coder: RSCoder, pairs, decode_indexes, erased, mode: int = _l
         raise ValueError("decode_indexes needs exactly k entries")
     arr = (_lib.BatchT * max(1, len(pairs)))()
     for i, (inputs, outputs) in enumerate(pairs):
-        B, _, L = inputs.shape
+        B, L = _decode_shapes(coder, inputs, decode_indexes, erased, outputs, inputs_by_unit, outputs_by_unit)
         arr[i] = _lib.BatchT(L, B, _shards(inputs), _shards(outputs))
     flags = (_lib.INPUTS_BY_UNIT if inputs_by_unit else 0) | (_lib.OUTPUTS_BY_UNIT if outputs_by_unit else 0)
     return check(lib.elect_ec_decode_batches(coder.handle, arr, len(pairs), int_array(decode_indexes),
@@ -236,7 +257,11 @@ def apply_batch(coef: np.ndarray, src, dst, stream=None) -> None:
     """dst[r] = XOR_j coef[r, j] * src[j] over [B, L] column tensors."""
     coef = np.ascontiguousarray(coef, np.uint8)
     rows, cols = coef.shape
+    if len(src) != cols or len(dst) != rows:
+        raise ValueError(f"apply_batch: {cols} source and {rows} output columns expected, got {len(src)} / {len(dst)}")
     B, L = src[0].shape
+    if any(t.dim() != 2 or tuple(t.shape) != (B, L) for t in list(src) + list(dst)):
+        raise ValueError(f"apply_batch: every column must be [{B}, {L}]")
     s = (ColumnT * cols)(*[_column(t) for t in src])
     d = (ColumnT * rows)(*[_column(t) for t in dst])
     check(lib.elect_ec_apply_batch(coef.ctypes.data_as(_lib._u8p), rows, cols, L, B, s, d, _stream(stream)),

@@ -200,3 +200,28 @@ def test_partition_by_bytes():
         for r in range(world):
             b, e = partition_by_bytes(sizes, world, r)
             assert e - b == 4096 // world
+
+
+def test_device_api_rejects_mismatched_shapes():
+    """The device-resident wrappers check every tensor's shape before the C ABI
+    sees its strides: an output with another stripe count or chunk length (a
+    tiled coding view decoded into a [B, 1, L] buffer, say) would otherwise be
+    written out of bounds on the device.  Raised before any device call."""
+    import torch
+    from elect_amd.batch import apply_batch, decode_batch, decode_batches, encode_update_batch
+    from elect_amd.coder import RSCoder
+    import numpy as np
+    c = RSCoder(4, 2)
+    st = torch.zeros((16, 6, 64), dtype=torch.uint8)
+    with pytest.raises(ValueError, match="outputs"):
+        decode_batch(c, st, [1, 2, 3, 4], [0], torch.zeros((1, 1, 1024), dtype=torch.uint8), inputs_by_unit=True)
+    with pytest.raises(ValueError, match="outputs"):
+        decode_batch(c, st, [1, 2, 3, 4], [0, 5], st[:, :3], outputs_by_unit=True, inputs_by_unit=True)
+    with pytest.raises(ValueError, match="inputs"):
+        decode_batch(c, st[:, :3], [0, 1, 2, 3], [4], torch.zeros((16, 1, 64), dtype=torch.uint8))
+    with pytest.raises(ValueError, match="outputs"):
+        decode_batches(c, [(st, torch.zeros((16, 1, 32), dtype=torch.uint8))], [1, 2, 3, 4], [0], inputs_by_unit=True)
+    with pytest.raises(ValueError, match="parity_out"):
+        encode_update_batch(c, 0, st[:, 0], st[:, 1], st[:, 4:], torch.zeros((8, 2, 64), dtype=torch.uint8))
+    with pytest.raises(ValueError, match="apply_batch"):
+        apply_batch(np.ones((1, 2), np.uint8), [st[:, 0], st[:2, 1]], [st[:, 4]])
