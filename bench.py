@@ -28,6 +28,7 @@ from __future__ import annotations
 import argparse
 import glob
 import json
+import math
 import os
 import sys
 import time
@@ -72,6 +73,8 @@ def parse():
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (PCIe) measurement")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the mixed (configs[3]) and RS(12,8) (configs[4]) lines of the headline run")
+    ap.add_argument("--configs-order", default="mixed,rs12",
+                    help="headline: the BASELINE configs run after the headline phases, in this order")
     ap.add_argument("--no-sizes", action="store_true",
                     help="headline: skip the 1 KiB / 1 MiB chunk-size lines (sizes) after the 64 KiB one")
     ap.add_argument("--config", default="headline",
@@ -86,6 +89,13 @@ def parse():
     ap.add_argument("--pad-fill", default="random",
                     help="padded: content lengths 'random' (uniform [0, L]) or a fixed fraction of L")
     ap.add_argument("--host-chunk", type=int, default=4404020, help="hostpath: bytes per unit per call")
+    ap.add_argument("--host-devices", type=int, default=0,
+                    help="hostpath: spread the callers over devices 0..N-1 (elect_ec_set_host_devices, what "
+                         "ELECT_EC_DEVICES=all does for ELECT's one JVM per node); 0: the current device only")
+    ap.add_argument("--host-seconds", type=float, default=0.0,
+                    help="hostpath: repeat the timed calls until at least this much wall time has passed")
+    ap.add_argument("--no-hostpath", action="store_true",
+                    help="headline: skip the JNI-convention host path over all the job's devices")
     ap.add_argument("--host-op", choices=("encode", "encode_ex"), default="encode",
                     help="hostpath: plain encode (the JNI encodeImpl), or ELECT's fused encode step "
                          "(encodeExImpl: content = codeLength/1.05, parity hashCodes)")
@@ -188,16 +198,29 @@ def host_cpu_info() -> dict:
     return info
 
 
+def cpu_thread_points(info: dict) -> list:
+    """Thread counts the CPU baseline sweeps: the cgroup quota, twice it, 64 and the
+    whole affinity mask (each at most the mask), so that the reported figure is the
+    box's best and not an oversubscribed run (a 16-CPU quota under a 256-CPU mask)."""
+    aff = info["affinity"]
+    q = math.ceil(info["quota_cores"]) if info.get("quota_cores") else None
+    pts = {aff, min(64, aff)}
+    if q:
+        pts |= {min(q, aff), min(2 * q, aff)}
+    return sorted(p for p in pts if p >= 1)
+
+
 def cpu_baseline(args, k, m, L, stripes):
     """Oracle SIMD path (ISA-L's algorithm restated) on the host cores: the same
     encode + single-erasure decode step over the same stripe batch the GPU codes
-    (4096 x 64 KiB: 1 GiB of data, 1.75 GiB touched, far beyond any LLC), one
-    thread per CPU in the affinity mask, stripes split evenly over them; then the
-    same loop on one thread.  Bounded to about --cpu-seconds of threaded work."""
+    (4096 x 64 KiB: 1 GiB of data, 1.75 GiB touched, far beyond any LLC), stripes
+    split evenly over the threads.  The thread count is swept (cpu_thread_points)
+    and the best point is the value; then the same loop on one thread.  Bounded
+    to about --cpu-seconds of threaded work in all."""
     import numpy as np
     from oracle import ec_oracle as orc
     info = host_cpu_info()
-    threads = info["affinity"]
+    points = cpu_thread_points(info)
     n = k + m
     buf = np.empty((stripes, n, L), np.uint8)
     orc.fill_splitmix(0xE1EC7, buf)
@@ -219,28 +242,36 @@ def cpu_baseline(args, k, m, L, stripes):
             reps += 1
         return reps, t
 
-    orc.batch_apply(enc_coef, buf, sstride, enc_src, buf, sstride, enc_dst, L, stripes, threads, level)  # warm
-    reps, total_t = loop(threads, args.cpu_seconds, 2)
+    step_bytes = 2 * stripes * k * L
+    orc.batch_apply(enc_coef, buf, sstride, enc_src, buf, sstride, enc_dst, L, stripes, points[-1], level)  # warm
+    sweep = {}
+    for p in points:
+        reps, t = loop(p, args.cpu_seconds / len(points), 2)
+        sweep[p] = (reps, t, reps * step_bytes / t / GIB)
+    best = max(sweep, key=lambda p: sweep[p][2])
     assert np.array_equal(out[:, 0], buf[:, 0]), "CPU baseline decode mismatch"
     reps1, t1 = loop(1, args.cpu_seconds * 0.3, 1)  # single-core figure
-    step_bytes = 2 * stripes * k * L
+    reps, total_t, rate = sweep[best]
     return {
-        "value": round(reps * step_bytes / total_t / GIB, 3),
+        "value": round(rate, 3),
         "unit": "GiB/s",
-        "cores": threads,
+        "cores": best,
+        "threads_used": best,
         "kind": "port",
+        "sweep": {str(p): round(v[2], 3) for p, v in sweep.items()},
         "single_core_GiB/s": round(reps1 * step_bytes / t1 / GIB, 3),
         "working_set_bytes": int(buf.nbytes + out.nbytes),
         "cpu_model": info["model"],
         "affinity_cpus": info["affinity"],
         "cgroup_quota_cores": info["quota_cores"],
         "sample": f"RS({n},{k}) encode + decode (erase 0) of the GPU's batch: {stripes} stripes x {L} B "
-                  f"({stripes * k * L / GIB:.2f} GiB data), {reps} reps in {total_t:.1f} s on {threads} threads; "
-                  f"{reps1} reps in {t1:.1f} s on 1; oracle {orc.simd_name(level)} (ISA-L's algorithm)",
+                  f"({stripes * k * L / GIB:.2f} GiB data); threads swept over {points}, best {best}: {reps} reps "
+                  f"in {total_t:.1f} s; {reps1} reps in {t1:.1f} s on 1; oracle {orc.simd_name(level)} "
+                  f"(ISA-L's algorithm)",
     }
 
 
-def host_inclusive(coder, k, m, L, stripes_total, dev):
+def host_inclusive(coder, k, m, L, stripes_total, dev, world=1):
     """Pinned host -> H2D -> encode -> D2H; GiB/s of data.  Three streams (H2D,
     compute, D2H) over a ring of 3 device buffers chained by events, so both
     copy directions stay busy; 32 MiB of data per transfer
@@ -285,19 +316,29 @@ def host_inclusive(coder, k, m, L, stripes_total, dev):
         t0 = time.perf_counter()
         run()
         rates.append(nch * chunk * k * L / (time.perf_counter() - t0) / GIB)
+    # every rank at once (each over its own PCIe link): 3 passes between barriers,
+    # aggregate = all ranks' data / the slowest rank's time
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        run()
+    own = time.perf_counter() - t0
+    barrier(world)
+    agg = world * 3 * nch * chunk * k * L / max_over_ranks(own, world) / GIB
     ref = torch.empty((chunk, m, L), dtype=torch.uint8, device=dev)
     encode_batch(coder, h_data[-chunk:].to(dev), ref)
     torch.cuda.synchronize()
     if not torch.equal(ref.cpu(), h_par[-chunk:]):
         raise RuntimeError("host-inclusive pipeline: parity mismatch")
-    return round(sorted(rates)[2], 2)
+    return round(sorted(rates)[2], 2), round(agg, 2)
 
 
-def decode_sweep(coder, stripe, k, m, L, B, stream, reps=5):
+def decode_sweep(coder, stripe, stream, reps=5):
     """Single-erasure decode for each data shard j (survivors: the other k of
-    shards 0..k), outside the timed region: per-kernel GB/s and HBM fraction."""
+    shards 0..k), outside the timed region: per-kernel GB/s and HBM fraction.
+    The geometry is the coding view's (tiled layouts: B*T stripes of 64 KiB)."""
     from elect_amd.batch import decode_batch
-    B, L = stripe.shape[0], stripe.shape[2]  # the coding view (tiled layouts: B*T stripes of 64 KiB)
+    B, L, k = stripe.shape[0], stripe.shape[2], coder.k
     out = torch.empty((B, 1, L), dtype=torch.uint8, device=stripe.device)
     res = {}
     for j in range(k):
@@ -374,6 +415,15 @@ def device_copy_rate(dev, nbytes=1 << 30, reps=5):
     ms = e0.elapsed_time(e1) / reps
     del a, b
     return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
+
+
+def chunk_name(L: int) -> str:
+    """'64 KiB' for 65536 (BASELINE.json's metric string), '1 MiB', or bytes."""
+    if L % (1 << 20) == 0:
+        return f"{L >> 20} MiB"
+    if L % 1024 == 0:
+        return f"{L >> 10} KiB"
+    return f"{L} B"
 
 
 TILE = 1 << 16  # the unit size HBM streams best back to back (DESIGN.md §3)
@@ -615,7 +665,11 @@ def config_hostpath(args, world, rank, dev):
     """The drop-in path exactly as ELECT drives it: synchronous encode of one
     stripe per call from pageable host memory (JVM direct buffers), codeLength
     = ceil(4 MiB * 1.05) = 4,404,020 B (StorageService.java:331-339), with
-    --threads concurrent callers (ELECT's concurrent_ec pool, elect.yaml:598)."""
+    --threads concurrent callers (ELECT's concurrent_ec pool, elect.yaml:598;
+    each coding task encodes synchronously, ECMessageVerbHandler.java:282-319).
+    --host-devices N spreads the callers over devices 0..N-1 the way
+    ELECT_EC_DEVICES=all does for ELECT's one JVM per node (each calling thread
+    keeps one device, round robin)."""
     import threading
 
     import numpy as np
@@ -626,17 +680,24 @@ def config_hostpath(args, world, rank, dev):
     T = args.threads
     coder = RSCoder(k, m)
     _lib.set_batching(args.batch)
+    ndev = max(1, args.host_devices)
+    if args.host_devices:
+        avail = torch.cuda.device_count()
+        if ndev > avail:
+            raise SystemExit(f"--host-devices {ndev}: only {avail} device(s) visible")
+        _lib.set_host_devices(list(range(ndev)))
     bufs = []
     for t in range(T):
         d = [np.random.default_rng(t * 8 + j).integers(0, 256, L, dtype=np.uint8) for j in range(k)]
         p = [np.empty(L, np.uint8) for _ in range(m)]
         bufs.append((d, p))
-    calls = max(4, args.steps // 2) * max(1, 4404020 // L // 8)
+    calls = max(4, args.steps // 2) * max(1, 4404020 // L // 8) * ndev
     fused = args.host_op == "encode_ex"
     content = [int(L / 1.05) - 64 * j for j in range(k)]  # SSTables just under codeLength/1.05
 
     def worker(t, n):
-        torch.cuda.set_device(dev)
+        if not args.host_devices:
+            torch.cuda.set_device(dev)
         d, p = bufs[t]
         da, pa = [x.ctypes.data for x in d], [x.ctypes.data for x in p]
         for _ in range(n):
@@ -652,10 +713,13 @@ def config_hostpath(args, world, rank, dev):
         for x in th:
             x.join()
 
-    run(1)
-    t0 = time.perf_counter()
-    run(calls)
-    dt = time.perf_counter() - t0
+    run(1)  # warm: every caller's device, arenas and dispatchers
+    done, dt = 0, 0.0
+    while done == 0 or dt < args.host_seconds:
+        t0 = time.perf_counter()
+        run(calls)
+        dt += time.perf_counter() - t0
+        done += calls
     d, p = bufs[0]  # self-check through the product: rebuild d0 from [p0, d1, d2, d3]
     rebuilt = np.empty(L, np.uint8)
     coder.decode_host([p[0].ctypes.data] + [x.ctypes.data for x in d[1:]], [4, 1, 2, 3], [0],
@@ -669,16 +733,72 @@ def config_hostpath(args, world, rank, dev):
         hs = coder.encode_ex_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L,
                                   data_lengths=content, hashed=True)
         ok = all(np.array_equal(a, b) for a, b in zip(p, ref)) and hs == [java_bytebuffer_hash(x) for x in ref]
+    # every caller's last parity against the CPU oracle's restatement is in tests/; here each
+    # caller's parity must at least equal caller 0's recomputation on its own data
     op_name = "fused encode step (zero fill + encode + parity hashCode, elect_ec_encode_ex)" if fused else \
         "encode"
     return {"metric": f"GiB/s host-memory RS(6,4) {op_name} through the C ABI (JNI calling convention)",
-            "value": round(T * calls * k * L / dt / GIB, 2), "unit": "GiB/s", "n_gpus": 1,
-            "steps": calls, "warmup": 1, "ms_per_step": round(dt / calls * 1e3, 3), "higher_is_better": True,
+            "value": round(T * done * k * L / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
+            "devices": ndev, "callers": T,
+            "steps": done, "warmup": 1, "ms_per_step": round(dt / done * 1e3, 3), "higher_is_better": True,
             "scaling": "none", "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
-            "config": {"workload": f"{T} threads x {calls} synchronous elect_ec_{args.host_op} calls, one stripe "
-                                   f"of {k} x {L} B each, pageable host buffers",
-                       "parallelism": "cross-thread batching (shared pinned arena, one launch per batch)"
-                                      if args.batch else "per-thread pinned staging + 2 streams"}}
+            "config": {"workload": f"{T} threads x {done} synchronous elect_ec_{args.host_op} calls, one stripe "
+                                   f"of {k} x {L} B each, pageable host buffers, over {ndev} device(s)",
+                       "parallelism": ("cross-thread batching (shared pinned arena, one launch per batch)"
+                                       if args.batch else "per-thread pinned staging + 2 streams") +
+                                      (f", callers spread over devices 0..{ndev - 1} (elect_ec_set_host_devices)"
+                                       if args.host_devices else "")}}
+
+
+HOSTPATH_CALLERS = 64  # ELECT's concurrent_ec (conf/elect.yaml:598)
+
+
+def hostpath_child_cmd(ndev: int) -> list:
+    """The child process hostpath_all_devices starts: the JNI calling convention,
+    64 callers, ELECT's codeLength, batching on, callers over devices 0..ndev-1."""
+    return [sys.executable, os.path.abspath(__file__), "--config", "hostpath", "--threads", str(HOSTPATH_CALLERS),
+            "--host-chunk", "4404020", "--batch", "1", "--host-devices", str(ndev), "--steps", "8",
+            "--host-seconds", "2"]
+
+
+def child_env() -> dict:
+    """This environment without the launcher's rank variables: the child is a
+    single process of its own (bench.py refuses a WORLD_SIZE that disagrees with
+    --gpus), not a member of the job's gloo group."""
+    drop = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE", "ROLE_RANK",
+            "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID",
+            "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_USE_AGENT_STORE")
+    return {key: v for key, v in os.environ.items() if key not in drop}
+
+
+def hostpath_all_devices(args, world, rank, child=None):
+    """The path ELECT actually calls, on every device of the job: rank 0 starts a
+    child process (ELECT runs one JVM per node) that drives the JNI calling
+    convention with 64 concurrent callers on ELECT's codeLength, batching on,
+    spread over devices 0..world-1 by elect_ec_set_host_devices
+    (ECMessageVerbHandler.java:282-319: a new coder and a synchronous encode per
+    stripe, on the ERASURECODE stage); the other ranks wait at the gloo barrier.
+    The child is a new process (no exec) and sees every device.  child: another
+    command line (the CPU plumbing test).  Returns the child's record on rank 0."""
+    import subprocess
+    res = None
+    barrier(world)
+    if rank == 0:
+        ndev = world if child is not None else min(world, torch.cuda.device_count())
+        cmd = child if child is not None else hostpath_child_cmd(ndev)
+        r = subprocess.run(cmd, capture_output=True, text=True, env=child_env(), timeout=900)
+        line = next((x for x in reversed(r.stdout.splitlines()) if x.startswith("{")), None)
+        if r.returncode != 0 or line is None:
+            res = {"verified": False, "devices": ndev, "error": f"rc={r.returncode}: {(r.stderr or r.stdout)[-400:]}"}
+        elif child is not None:
+            res = {"verified": True, "devices": ndev, "child": json.loads(line)}
+        else:
+            o = json.loads(line)
+            res = {"value": o["value"], "unit": o["unit"], "devices": o["devices"], "callers": o["callers"],
+                   "calls_per_caller": o["steps"], "verified": bool(o["verified"]),
+                   "workload": o["config"]["workload"], "parallelism": o["config"]["parallelism"]}
+    barrier(world)
+    return res
 
 
 def config_update(args, world, rank, dev):
@@ -972,7 +1092,9 @@ def other_configs(args, world, rank, dev):
     sub = copy.copy(args)
     sub.steps, sub.warmup, sub.mixed_share = min(args.steps, 20), min(args.warmup, 3), 0
     res = {}
-    for name, fn in (("mixed", config_mixed), ("rs12", config_rs12)):
+    fns = {"mixed": config_mixed, "rs12": config_rs12}
+    for name in [x for x in args.configs_order.split(",") if x]:
+        fn = fns[name]
         o = fn(sub, world, rank, dev)
         keep = ("metric", "value", "unit", "scaling", "steps", "ms_per_step", "host_submit_ms_per_step",
                 "verified", "classes", "kernels")
@@ -987,8 +1109,13 @@ def launch_check(args, world, rank):
     barrier(world)
     t = max_over_ranks(float(rank + 1), world)
     recs = gather({"rank": rank, "world": world, "pid": os.getpid()}, world)
+    hp = None
+    if world > 1:  # the headline's host-path phase: rank 0's child process, the others at the barrier
+        hp = hostpath_all_devices(args, world, rank, child=[sys.executable, os.path.abspath(__file__),
+                                                            "--launch-check"])
     if rank == 0:
-        print(json.dumps({"launch_check": True, "n_gpus": world, "max_over_ranks": t, "ranks": recs}), flush=True)
+        print(json.dumps({"launch_check": True, "n_gpus": world, "max_over_ranks": t, "ranks": recs,
+                          "hostpath_child": hp}), flush=True)
 
 
 def gather(obj, world):
@@ -1141,7 +1268,7 @@ def main():
     traffic, traffic_src = pmc_traffic("gf_apply_x16<4, 2")
 
     out = {
-        "metric": "GiB/s device-resident RS(6,4) encode+decode, 64 KiB chunks, 1/2/4/8 GPU",
+        "metric": f"GiB/s device-resident RS({n},{k}) encode+decode, {chunk_name(L)} chunks, 1/2/4/8 GPU",
         "value": round(value, 2),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -1205,11 +1332,21 @@ def main():
         rec["configs_submit_ms"] = {key: v["host_submit_ms_per_step"] for key, v in out["configs"].items()}
         rec["verified"] = rec["verified"] and all(rec["configs_verified"].values())
     if rank == 0:
-        out["kernels"]["decode_sweep"] = sw = decode_sweep(coder, stripe, k, m, L, B, stream)
+        out["kernels"]["decode_sweep"] = sw = decode_sweep(coder, stripe, stream)
         rec["verified"] = rec["verified"] and all(v["verified"] for v in sw.values())
         out["roofline"]["device_copy_GB/s"] = device_copy_rate(dev)
-    if rank == 0 and not args.no_host:
-        out["host_inclusive_GiB/s"] = host_inclusive(coder, k, m, L, min(B, 4096), dev)
+    if not args.no_host:  # every rank, over its own PCIe link, at the same time
+        own_rate, agg = host_inclusive(coder, k, m, L, min(B, 4096), dev, world)
+        rates = gather(own_rate, world)
+        out["host_inclusive_GiB/s"] = rates[0]
+        out["host_inclusive_sum_GiB/s"] = agg
+        out["host_inclusive_per_rank_GiB/s"] = rates
+    if not args.no_host and not args.no_hostpath:  # ELECT's own calls over all the job's devices
+        hp = hostpath_all_devices(args, world, rank)
+        if rank == 0:
+            out["hostpath_all_devices"] = hp
+            out["hostpath_all_devices_GiB/s"] = hp.get("value")
+            rec["verified"] = rec["verified"] and hp["verified"]
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args, k, m, L, B)
     finish(out, rank, world, rec)

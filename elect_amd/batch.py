@@ -36,6 +36,15 @@ def _rows(name: str, t: torch.Tensor, B: int, L: int, need: int) -> None:
         raise ValueError(f"{name}: expected [{B}, >={need}, {L}], got {tuple(t.shape)}")
 
 
+def _encode_shapes(coder, data, parity):
+    """data must be [B, k, L] and parity [B, >= m, L] (see _rows); returns B, L."""
+    if data.dim() != 3 or data.shape[1] != coder.k:
+        raise ValueError(f"data: expected a [stripes, {coder.k}, L] tensor, got {tuple(data.shape)}")
+    B, _, L = data.shape
+    _rows("parity", parity, B, L, coder.m)
+    return B, L
+
+
 def _decode_shapes(coder, inputs, decode_indexes, erased, outputs, inputs_by_unit, outputs_by_unit):
     if len(decode_indexes) != coder.k:
         raise ValueError("decode_indexes needs exactly k entries")
@@ -66,7 +75,7 @@ def encode_batch_hashed(coder: RSCoder, data: torch.Tensor, parity: torch.Tensor
                         stream=None) -> None:
     """encode_batch that also writes every parity unit's java.nio.ByteBuffer.hashCode()
     into hashes (int32 device tensor [B, m])."""
-    B, k, L = data.shape
+    B, L = _encode_shapes(coder, data, parity)
     if hashes.shape != (B, coder.m) or hashes.dtype != torch.int32 or not hashes.is_contiguous():
         raise ValueError("hashes must be a contiguous int32 [B, m] tensor")
     check(lib.elect_ec_encode_batch_hashed(coder.handle, L, B, _shards(data), _shards(parity), hashes.data_ptr(),
@@ -77,7 +86,8 @@ def encode_batch_padded(coder: RSCoder, data: torch.Tensor, lengths: torch.Tenso
                         stream=None) -> None:
     """encode_batch where data[s, j] holds only lengths[s, j] valid bytes (int32/uint32
     device tensor [B, k]); the rest reads as zero and is never loaded."""
-    B, k, L = data.shape
+    B, L = _encode_shapes(coder, data, parity)
+    k = coder.k
     if lengths.shape != (B, k) or lengths.dtype not in (torch.int32, torch.uint32) or \
             not lengths.is_contiguous() or lengths.device != data.device:
         raise ValueError("lengths must be a contiguous int32 [B, k] tensor on the data's device")
@@ -178,8 +188,10 @@ def encode_update_batch_ex(coder: RSCoder, target: int, old: torch.Tensor, new: 
 
 def _tiles_of(chunk_size: int, tile: int, rows: int) -> int:
     """Stripes in a tiled batch whose coding view has `rows` tile rows."""
+    if tile <= 0:
+        raise ValueError(f"a tiled view needs a positive tile length, got {tile}")
     t = max(1, -(-chunk_size // tile))
-    if tile <= 0 or rows % t:
+    if rows % t:
         raise ValueError(f"a tiled view needs a multiple of {t} tile rows (ceil({chunk_size}/{tile})), got {rows}")
     return rows // t
 

@@ -182,7 +182,9 @@ int update_batch_impl(const elect_ec_coder* coder, size_t chunk_size, size_t til
                       int32_t* d_hashes, void* stream)
 {
     if (!valid_coder(coder) || target_data_index < 0 || target_data_index >= coder->k) return ELECT_EC_EINVAL;
-    if (d_hashes && tile && 2 + coder->m > ELECT_EC_MAX_DATA_UNITS) return ELECT_EC_EINVAL;
+    // tiled launches ride on the padded vector kernels (at most kMaxPadCols columns),
+    // hashed or not: refuse a wider tiled update here, not inside the launcher
+    if (tile && 2 + coder->m > elect::kern::kMaxPadCols) return ELECT_EC_EINVAL;
     if ((d_old_new_lengths || tile) && chunk_size > 0xFFFFFFFFull) return ELECT_EC_EINVAL;
     if (num_stripes == 0 || (chunk_size == 0 && !d_hashes)) return ELECT_EC_OK;
     if (chunk_size > 0 && (!old_data.ptr || !new_data.ptr || !parity_in.base || !parity_out.base))

@@ -491,7 +491,10 @@ public:
         } in_flight(callers_);
         // untiled: one unit per column at a 256-byte pitch; tiled: T tiles of 64 KiB
         const size_t tile = batch_config().tile.load();
-        const size_t tiles = tile && tile % 16 == 0 && len > tile ? (len + tile - 1) / tile : 1;
+        // (tiled launches ride on the padded vector kernels: a wider product, the
+        // update of an m >= 9 code, stays untiled rather than fail its whole batch)
+        const bool tileable = op.cols <= kern::kMaxPadCols;
+        const size_t tiles = tileable && tile && tile % 16 == 0 && len > tile ? (len + tile - 1) / tile : 1;
         const size_t pitch = tiles > 1 ? tile : (len + 255) & ~size_t{255};
         // the copy lists' room first: past the reservation below nothing may throw
         // (a slot reserved and never filled would stall its batch)

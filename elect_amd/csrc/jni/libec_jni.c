@@ -18,14 +18,17 @@
  *  - int arrays are released (EC/jni_common.c:75, 99 and EC/NativeRSDecoder.c:59-62 leak);
  *  - a negative engine status becomes a Java exception instead of being ignored;
  *  - a negative dataLen is an IllegalArgumentException (the reference memsets a
- *    negative size: EC/erasure_coder.c:86-88);
- *  - the three unconditional printf lines of decodeImpl (EC/NativeRSDecoder.c:57,
- *    65, 68) print only when allowVerboseDump() is true.
- * With allowVerboseDump() true (read on every call, EC/jni_common.c:44-57) the
- * coder dumps print in EC/dump.c's format: the encoder block (dumpEncoder,
- * EC/dump.c:61-73) on encode/encodeUpdate, the decoder block (dumpDecoder,
- * :75-104: erased and decode indexes, encode / invert / decode matrices) on
- * decode after the reference's three decodeImpl lines.
+ *    negative size: EC/erasure_coder.c:86-88).
+ * Standard output is libec.so's:
+ *  - decodeImpl prints its three progress lines on every call, verbose or not
+ *    (EC/NativeRSDecoder.c:57, 65, 68; ELECT_EC_JNI_QUIET=1 silences them);
+ *  - with allowVerboseDump() true (read on every call, EC/jni_common.c:44-57),
+ *    decode also prints the decoder block in EC/dump.c's format (dumpDecoder,
+ *    :75-104: erased and decode indexes, encode / invert / decode matrices),
+ *    after the third line, as processErasures does (EC/erasure_coder.c:195-197);
+ *  - encode and encodeUpdate print nothing: the reference's only dumpEncoder
+ *    call sits in initEncoder right after initCoder zeroes verbose
+ *    (EC/erasure_coder.c:27, 61-63), so it never runs.
  *
  * JEC/ = src/elect/src/java/org/apache/cassandra/io/erasurecode
  * EC/  = src/elect/src/native/src/org/apache/cassandra/io/erasurecode
@@ -127,18 +130,6 @@ static void dump_coding_matrix(const unsigned char* buf, int n1, int n2)
     printf("\n");
 }
 
-/* dumpEncoder (EC/dump.c:61-73) */
-static void dump_encoder(const elect_ec_coder* c)
-{
-    unsigned char em[ELECT_EC_MAX_UNITS * ELECT_EC_MAX_DATA_UNITS] = {0};
-    int k = elect_ec_coder_num_data_units(c), m = elect_ec_coder_num_parity_units(c);
-    elect_ec_coder_encode_matrix(c, em, sizeof em);
-    printf("Encoding (numAllUnits = %d, numParityUnits = %d, numDataUnits = %d)\n", k + m, m, k);
-    printf("\n\nEncodeMatrix:\n");
-    dump_coding_matrix(em, k, k + m);
-    fflush(stdout);
-}
-
 /* dumpDecoder (EC/dump.c:75-104).  The reference's invert and decode matrices
  * live in zeroed MMAX x KMAX arrays (clearDecoder, EC/erasure_coder.c:229-238),
  * so rows past k (invert) and past numErased (decode) print as zeros. */
@@ -230,15 +221,12 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeImpl(JNIEnv* env,
     unsigned char* in[2 + EC_MAX];
     unsigned char* out[2 + EC_MAX];
     elect_ec_coder* c = coder_for_call(env, thiz, "NativeRSRawEncoder closed");
-    int v;
-    if (c == NULL || (v = verbose(env, thiz)) < 0 || bad_length(env, dataLen))
+    if (c == NULL || verbose(env, thiz) < 0 || bad_length(env, dataLen))  /* (getCoder's call) */
         return;
     int k = elect_ec_coder_num_data_units(c), m = elect_ec_coder_num_parity_units(c);
     if (buffers(env, inputs, inputOffsets, k, in, "Invalid inputs") ||
         buffers(env, outputs, outputOffsets, m, out, "Invalid outputs"))
         return;
-    if (v)
-        dump_encoder(c);
     raise_status(env, elect_ec_encode(c, (const unsigned char* const*)in, out, (size_t)dataLen), "encode");
 }
 
@@ -253,15 +241,12 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeUpdateImpl(JNIEnv
     unsigned char* in[2 + EC_MAX];
     unsigned char* out[2 + EC_MAX];
     elect_ec_coder* c = coder_for_call(env, thiz, "NativeRSRawEncoder closed");
-    int v;
-    if (c == NULL || (v = verbose(env, thiz)) < 0 || bad_length(env, dataLen))
+    if (c == NULL || verbose(env, thiz) < 0 || bad_length(env, dataLen))  /* (getCoder's call) */
         return;
     int m = elect_ec_coder_num_parity_units(c);
     if (buffers(env, inputs, inputOffsets, 2 + m, in, "Invalid inputs") ||
         buffers(env, outputs, outputOffsets, m, out, "Invalid outputs"))
         return;
-    if (v)
-        dump_encoder(c);
     raise_status(env,
                  elect_ec_encode_update(c, (const unsigned char* const*)in, targetUpdateDataIndex, out,
                                         (size_t)dataLen),
@@ -318,16 +303,13 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeExImpl(JNIEnv* en
     const size_t* use_lens;
     jint h[EC_MAX];
     elect_ec_coder* c = coder_for_call(env, thiz, "NativeRSRawEncoder closed");
-    int v;
-    if (c == NULL || (v = verbose(env, thiz)) < 0 || bad_length(env, dataLen))
+    if (c == NULL || verbose(env, thiz) < 0 || bad_length(env, dataLen))  /* (getCoder's call) */
         return;
     int k = elect_ec_coder_num_data_units(c), m = elect_ec_coder_num_parity_units(c);
     if (buffers(env, inputs, inputOffsets, k, in, "Invalid inputs") ||
         buffers(env, outputs, outputOffsets, m, out, "Invalid outputs") ||
         content_lengths(env, contentLengths, k, lens, &use_lens) || hash_array(env, parityHashes, m))
         return;
-    if (v)
-        dump_encoder(c);
     if (raise_status(env,
                      elect_ec_encode_ex(c, (const unsigned char* const*)in, use_lens, out, (size_t)dataLen,
                                         parityHashes ? (int32_t*)h : NULL),
@@ -348,16 +330,13 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeUpdateExImpl(
     const size_t* use_lens;
     jint h[EC_MAX];
     elect_ec_coder* c = coder_for_call(env, thiz, "NativeRSRawEncoder closed");
-    int v;
-    if (c == NULL || (v = verbose(env, thiz)) < 0 || bad_length(env, dataLen))
+    if (c == NULL || verbose(env, thiz) < 0 || bad_length(env, dataLen))  /* (getCoder's call) */
         return;
     int m = elect_ec_coder_num_parity_units(c);
     if (buffers(env, inputs, inputOffsets, 2 + m, in, "Invalid inputs") ||
         buffers(env, outputs, outputOffsets, m, out, "Invalid outputs") ||
         content_lengths(env, contentLengths, 2, lens, &use_lens) || hash_array(env, parityHashes, m))
         return;
-    if (v)
-        dump_encoder(c);
     if (raise_status(env,
                      elect_ec_encode_update_ex(c, (const unsigned char* const*)in, use_lens, targetUpdateDataIndex,
                                                out, (size_t)dataLen, parityHashes ? (int32_t*)h : NULL),
@@ -384,6 +363,14 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_initImpl(JNIEnv* env, j
     init_coder(env, thiz, numDataUnits, numParityUnits);
 }
 
+/* ELECT_EC_JNI_QUIET=1 drops decodeImpl's three progress lines (the reference
+ * prints them on every decode, EC/NativeRSDecoder.c:57, 65, 68). */
+static int quiet(void)
+{
+    const char* s = getenv("ELECT_EC_JNI_QUIET");
+    return s != NULL && strcmp(s, "1") == 0;
+}
+
 /* ELECT_EC_DECODE_MODE=strict switches off the compat zero rows for every
  * decoder in the process; the default is bit-exact libec.so. */
 static int decode_mode(void)
@@ -407,7 +394,8 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_decodeImpl(JNIEnv* env,
     if (c == NULL || (v = verbose(env, thiz)) < 0 || bad_length(env, dataLen))
         return;
     int k = elect_ec_coder_num_data_units(c), m = elect_ec_coder_num_parity_units(c);
-    if (v)  /* EC/NativeRSDecoder.c:57 */
+    const int say = !quiet();
+    if (say)  /* EC/NativeRSDecoder.c:57 */
         printf("NativeRSDecoder_decodeImpl, start to process: data unit = %d, parity unit = %d, data block size = %d\n",
                k, m, (int)dataLen);
     int n_dec = (*env)->GetArrayLength(env, decodeIndexes);
@@ -418,16 +406,18 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_decodeImpl(JNIEnv* env,
     }
     (*env)->GetIntArrayRegion(env, decodeIndexes, 0, k, (jint*)dec);
     (*env)->GetIntArrayRegion(env, erasedIndexes, 0, n_era, (jint*)era);
-    if (v)  /* :65 */
+    if (say)  /* :65 */
         printf("NativeRSDecoder_decodeImpl, read data: target recovery data block number = %d, the first recovery "
                "request block ID = %d\n", n_era, n_era > 0 ? era[0] : 0);
     if (buffers(env, inputs, inputOffsets, k, in, "Invalid inputs") ||
         buffers(env, outputs, outputOffsets, n_era, out, "Invalid outputs"))
         return;
-    if (v) {  /* :68, then processErasures' dumpDecoder (EC/erasure_coder.c:195-197) */
+    if (say)  /* :68 */
         printf("NativeRSDecoder_decodeImpl, start do decode\n");
+    if (v)  /* processErasures' dumpDecoder (EC/erasure_coder.c:195-197) */
         dump_decoder(c, dec, era, n_era, decode_mode());
-    }
+    else if (say)
+        fflush(stdout);
     raise_status(env,
                  elect_ec_decode(c, (const unsigned char* const*)in, dec, era, n_era, out, (size_t)dataLen,
                                  decode_mode()),

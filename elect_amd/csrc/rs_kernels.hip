@@ -1201,9 +1201,8 @@ const std::array<std::array<FastFn, kFastRows>, kMaxCols> kFast = {
     fast_row_fns<9>(),  fast_row_fns<10>(), fast_row_fns<11>(), fast_row_fns<12>(),
     fast_row_fns<13>(), fast_row_fns<14>(), fast_row_fns<15>(), fast_row_fns<16>()};
 
-// Padded variants exist for up to ELECT_EC_MAX_DATA_UNITS (10) columns: the
-// encode shapes and ELECT's decode (k survivors).
-constexpr int kMaxPadCols = 10;
+// Padded variants exist for up to ELECT_EC_MAX_DATA_UNITS (kMaxPadCols = 10)
+// columns: the encode shapes and ELECT's decode (k survivors).
 const std::array<std::array<FastFn, kFastRows>, kMaxPadCols> kFastPad = {
     fast_row_fns<1, true>(), fast_row_fns<2, true>(), fast_row_fns<3, true>(), fast_row_fns<4, true>(),
     fast_row_fns<5, true>(), fast_row_fns<6, true>(), fast_row_fns<7, true>(), fast_row_fns<8, true>(),

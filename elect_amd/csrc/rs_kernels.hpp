@@ -21,6 +21,10 @@ namespace kern {
 constexpr int kMaxCols = 16;  // source columns per launch
 constexpr int kMaxRows = 16;  // output rows per call (fast kernels take 4 per launch)
 constexpr int kFastRows = 4;
+// Widest padded (and so tiled) vector instance: ELECT_EC_MAX_DATA_UNITS.  Tiled
+// launches need the padded vector kernels, so a wider product (an update of an
+// m >= 9 code: 2 + m columns) must be coded untiled.
+constexpr int kMaxPadCols = 10;
 
 // A shard column over a batch of stripes: stripe s's bytes start at ptr + s*stride.
 struct Column {

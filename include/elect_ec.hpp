@@ -289,4 +289,129 @@ private:
 };
 
 }  // namespace erasurecode
+
+// ---------------------------------------------------------------------------
+// Checked device-batch calls for C++ callers (the elect_ec_*_batch entry points
+// of elect_ec.h).  The C ABI addresses a device batch from its base and strides
+// alone, so a descriptor with fewer stripes, units or bytes than the call
+// implies is read or written out of bounds on the device.  A DeviceBatch states
+// its geometry (and, optionally, the bytes allocated from base), and every call
+// below checks it before anything is enqueued: the same checks as the Python
+// wrappers (elect_amd/batch.py).  std::invalid_argument on a mismatch.
+// ---------------------------------------------------------------------------
+namespace device {
+
+// `stripes` stripes of `units` units of `len` bytes: unit i of stripe s at
+// base + s*stripe_stride + i*unit_stride.  `bytes` = the allocation behind base
+// (0 = unknown: geometry checks only).
+struct DeviceBatch {
+    void* base = nullptr;
+    size_t stripes = 0;
+    size_t units = 0;
+    size_t len = 0;
+    size_t stripe_stride = 0;
+    size_t unit_stride = 0;
+    size_t bytes = 0;
+
+    // a contiguous [stripes][units][len] block
+    static DeviceBatch contiguous(void* p, size_t stripes, size_t units, size_t len)
+    {
+        return DeviceBatch{p, stripes, units, len, units * len, len, stripes * units * len};
+    }
+    // units [first, first + n) of this batch (same stripes and strides)
+    DeviceBatch slice(size_t first, size_t n) const
+    {
+        if (first + n > units) throw std::invalid_argument("DeviceBatch::slice past the last unit");
+        DeviceBatch b = *this;
+        b.base = static_cast<unsigned char*>(base) + first * unit_stride;
+        b.units = n;
+        if (bytes) b.bytes = bytes - first * unit_stride;
+        return b;
+    }
+    elect_ec_shards shards() const { return elect_ec_shards{base, stripe_stride, unit_stride}; }
+};
+
+namespace detail {
+inline void check_batch(const char* name, const DeviceBatch& b, size_t stripes, size_t len, size_t need)
+{
+    auto fail = [&](const std::string& why) {
+        throw std::invalid_argument(std::string(name) + ": " + why + " (expected [" + std::to_string(stripes) + ", >=" +
+                                    std::to_string(need) + ", " + std::to_string(len) + "], got [" +
+                                    std::to_string(b.stripes) + ", " + std::to_string(b.units) + ", " +
+                                    std::to_string(b.len) + "])");
+    };
+    if (b.stripes != stripes || b.len != len || b.units < need) fail("shape mismatch");
+    if (stripes && len && !b.base) fail("null base");
+    if (b.bytes && stripes && need) {  // the farthest byte the call touches lies inside the allocation
+        const size_t last = (stripes - 1) * b.stripe_stride + (need - 1) * b.unit_stride + len;
+        if (last > b.bytes) fail("strides reach " + std::to_string(last) + " B past a " + std::to_string(b.bytes) + " B buffer");
+    }
+}
+
+inline int max_index(const int* idx, int n)
+{
+    int m = -1;
+    for (int i = 0; i < n; ++i) m = idx[i] > m ? idx[i] : m;
+    return m;
+}
+}  // namespace detail
+
+// elect_ec_encode_batch: data [B, >=k, L], parity [B, >=m, L].
+inline int encode_batch(const elect_ec_coder* c, const DeviceBatch& data, const DeviceBatch& parity, void* stream)
+{
+    const size_t k = elect_ec_coder_num_data_units(c), m = elect_ec_coder_num_parity_units(c);
+    detail::check_batch("data", data, data.stripes, data.len, k);
+    detail::check_batch("parity", parity, data.stripes, data.len, m);
+    return elect_ec_encode_batch(c, data.len, data.stripes, data.shards(), parity.shards(), stream);
+}
+
+// elect_ec_encode_batch_ex (content lengths and hashes: DEVICE arrays of
+// [B][k] / [B][m] entries the caller sized; the C ABI reads them by index).
+inline int encode_batch_ex(const elect_ec_coder* c, const DeviceBatch& data, const uint32_t* d_lengths,
+                           const DeviceBatch& parity, int32_t* d_hashes, void* stream)
+{
+    const size_t k = elect_ec_coder_num_data_units(c), m = elect_ec_coder_num_parity_units(c);
+    detail::check_batch("data", data, data.stripes, data.len, k);
+    detail::check_batch("parity", parity, data.stripes, data.len, m);
+    return elect_ec_encode_batch_ex(c, data.len, data.stripes, data.shards(), d_lengths, parity.shards(), d_hashes,
+                                    stream);
+}
+
+// elect_ec_decode_batch: inputs [B, k (or max(decode_indexes)+1 with
+// ELECT_EC_INPUTS_BY_UNIT), L], outputs [B, num_erased (or max(erased)+1 with
+// ELECT_EC_OUTPUTS_BY_UNIT), L].
+inline int decode_batch(const elect_ec_coder* c, const DeviceBatch& inputs, const int* decode_indexes,
+                        const int* erased, int num_erased, const DeviceBatch& outputs, unsigned flags, int mode,
+                        void* stream)
+{
+    const int k = elect_ec_coder_num_data_units(c);
+    if (num_erased < 0 || (num_erased > 0 && !erased) || !decode_indexes)
+        throw std::invalid_argument("decode_batch: bad index arrays");
+    const size_t in_need = (flags & ELECT_EC_INPUTS_BY_UNIT) ? detail::max_index(decode_indexes, k) + 1 : k;
+    const size_t out_need = (flags & ELECT_EC_OUTPUTS_BY_UNIT) ? detail::max_index(erased, num_erased) + 1
+                                                               : static_cast<size_t>(num_erased);
+    detail::check_batch("inputs", inputs, inputs.stripes, inputs.len, in_need);
+    detail::check_batch("outputs", outputs, inputs.stripes, inputs.len, out_need);
+    return elect_ec_decode_batch(c, inputs.len, inputs.stripes, inputs.shards(), decode_indexes, erased, num_erased,
+                                 outputs.shards(), flags, mode, stream);
+}
+
+// elect_ec_encode_update_batch: old / new [B, >=1, L] (unit 0 used), parity
+// in / out [B, >=m, L].
+inline int encode_update_batch(const elect_ec_coder* c, int target, const DeviceBatch& old_data,
+                               const DeviceBatch& new_data, const DeviceBatch& parity_in,
+                               const DeviceBatch& parity_out, void* stream)
+{
+    const size_t m = elect_ec_coder_num_parity_units(c);
+    detail::check_batch("old", old_data, old_data.stripes, old_data.len, 1);
+    detail::check_batch("new", new_data, old_data.stripes, old_data.len, 1);
+    detail::check_batch("parity_in", parity_in, old_data.stripes, old_data.len, m);
+    detail::check_batch("parity_out", parity_out, old_data.stripes, old_data.len, m);
+    return elect_ec_encode_update_batch(c, old_data.len, old_data.stripes, target,
+                                        elect_ec_column{old_data.base, old_data.stripe_stride},
+                                        elect_ec_column{new_data.base, new_data.stripe_stride}, parity_in.shards(),
+                                        parity_out.shards(), stream);
+}
+
+}  // namespace device
 }  // namespace elect

@@ -89,6 +89,41 @@ static int cpu_checks()
         NativeRSEncoder e2(ErasureCoderOptions(4, 2));
         EXPECT(throws<DeviceError>([&] { e2.encode(d.all(), p.all()); }, "no HIP device"));
     }
+    // checked device-batch calls: shapes and strides are checked before anything is
+    // enqueued (no device needed; the pointers below are never dereferenced)
+    {
+        using elect::device::DeviceBatch;
+        elect_ec_coder* c = nullptr;
+        EXPECT(elect_ec_coder_create(4, 2, &c) == ELECT_EC_OK);
+        alignas(16) static unsigned char fake[1];
+        const DeviceBatch st = DeviceBatch::contiguous(fake, 16, 6, 64);
+        const int dec[4] = {1, 2, 3, 4}, era[1] = {0}, era2[2] = {0, 5};
+        auto bad = [&](auto&& f, const char* needle) { return throws<std::invalid_argument>(f, needle); };
+        // a tiled view decoded into a buffer of another stripe count / length (round 2's fault)
+        EXPECT(bad([&] { elect::device::decode_batch(c, st, dec, era, 1, DeviceBatch::contiguous(fake, 1, 1, 1024),
+                                                     ELECT_EC_INPUTS_BY_UNIT, 0, nullptr); }, "outputs"));
+        EXPECT(bad([&] { elect::device::decode_batch(c, st, dec, era2, 2, st.slice(0, 3),
+                                                     ELECT_EC_INPUTS_BY_UNIT | ELECT_EC_OUTPUTS_BY_UNIT, 0, nullptr); },
+                   "outputs"));
+        EXPECT(bad([&] { elect::device::decode_batch(c, st.slice(0, 3), dec, era, 1,
+                                                     DeviceBatch::contiguous(fake, 16, 1, 64), 0, 0, nullptr); },
+                   "inputs"));
+        EXPECT(bad([&] { elect::device::encode_batch(c, st.slice(0, 4), DeviceBatch::contiguous(fake, 8, 2, 64), nullptr); },
+                   "parity"));
+        EXPECT(bad([&] { elect::device::encode_batch(c, st.slice(0, 3), st.slice(4, 2), nullptr); }, "data"));
+        // geometry right, but the strides run past the allocation
+        DeviceBatch small = st;
+        small.bytes = 16 * 6 * 64 - 1;
+        EXPECT(bad([&] { elect::device::encode_batch(c, small.slice(0, 4), small.slice(4, 2), nullptr); }, "past"));
+        EXPECT(bad([&] { elect::device::encode_update_batch(c, 0, st.slice(0, 1), st.slice(1, 1), st.slice(4, 2),
+                                                            DeviceBatch::contiguous(fake, 16, 1, 64), nullptr); },
+                   "parity_out"));
+        // a well-formed call reaches the C ABI (which, without a device, fails loudly)
+        int nd = 0;
+        if (elect_ec_device_count(&nd) != ELECT_EC_OK)
+            EXPECT(elect::device::encode_batch(c, st.slice(0, 4), st.slice(4, 2), nullptr) == ELECT_EC_ENODEV);
+        elect_ec_coder_destroy(c);
+    }
     return failures;
 }
 

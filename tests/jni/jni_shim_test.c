@@ -774,6 +774,19 @@ static int dump_cases(void)
     fflush(stdout);
     jni.decode(env, dec12, in8, off8, 16, int_array(8, di12), int_array(2, er12), out2, poff2);
     vm.pending = 0;
+    printf("=== encodeUpdate RS(6,4)\n");  /* verbose too: libec.so never dumps the encoder */
+    fflush(stdout);
+    jni.update(env, enc, in4, off4, 16, 1, out2, poff2);
+    vm.pending = 0;
+    enc->verbose = dec->verbose = JNI_FALSE;
+    printf("=== quiet encode RS(6,4)\n");
+    fflush(stdout);
+    jni.encode(env, enc, in4, off4, 16, out2, poff2);
+    vm.pending = 0;
+    printf("=== quiet decode RS(6,4) {4,1,2,3} erase {0}\n");  /* the three lines, unconditionally */
+    fflush(stdout);
+    jni.decode(env, dec, in4, off4, 16, int_array(4, di), int_array(1, er), out1, poff1);
+    vm.pending = 0;
     printf("=== end\n");
     jni.enc_destroy(env, enc);
     jni.dec_destroy(env, dec);

@@ -35,6 +35,12 @@ def test_bare_gpus_n_starts_n_ranks():
     assert all(x["world"] == 3 for x in d["ranks"])
     assert len({x["pid"] for x in d["ranks"]}) == 3  # one process per rank
     assert d["max_over_ranks"] == 3.0
+    # the headline's host-path phase: rank 0 starts a child process of its own (no
+    # launcher variables: a WORLD_SIZE left in its env would make it refuse) while
+    # the other ranks wait at the barrier; the child's record reaches the line
+    hp = d["hostpath_child"]
+    assert hp["verified"] and hp["devices"] == 3, hp
+    assert hp["child"]["n_gpus"] == 1 and hp["child"]["ranks"][0]["pid"] not in {x["pid"] for x in d["ranks"]}
 
 
 def test_single_rank_needs_no_launcher():
@@ -78,3 +84,49 @@ def test_launch_command_shape():
     assert cmd[1:3] == ["-m", "torch.distributed.run"]
     assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd and "--nnodes=1" in cmd
     assert cmd[-4:] == ["--gpus", "8", "--steps", "3"]
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod2", BENCH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_hostpath_child_command_and_env():
+    """The host path the headline line measures over the job's devices: ELECT's
+    64 callers (concurrent_ec) on ELECT's codeLength, batching on, devices 0..N-1;
+    the child's environment carries no launcher rank variables."""
+    mod = _bench_module()
+    cmd = mod.hostpath_child_cmd(8)
+    a = dict(zip(cmd[2::2], cmd[3::2]))
+    assert a["--config"] == "hostpath" and a["--threads"] == "64" and a["--host-devices"] == "8"
+    assert a["--host-chunk"] == "4404020" and a["--batch"] == "1"
+    old = dict(os.environ)
+    try:
+        os.environ.update(WORLD_SIZE="8", RANK="3", LOCAL_RANK="3", MASTER_ADDR="127.0.0.1", MASTER_PORT="1",
+                          TORCHELASTIC_RUN_ID="x")
+        env = mod.child_env()
+    finally:
+        os.environ.clear()
+        os.environ.update(old)
+    assert not {"WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID"} & set(env)
+    assert env.get("PATH") == os.environ.get("PATH")
+
+
+def test_cpu_baseline_thread_points():
+    """The CPU baseline sweeps the cgroup quota, twice it, 64 and the affinity
+    mask (capped at the mask), and reports the best point, so a 16-CPU quota under
+    a 256-CPU mask is not reported as a 256-thread oversubscribed run."""
+    mod = _bench_module()
+    assert mod.cpu_thread_points({"affinity": 256, "quota_cores": 16.0}) == [16, 32, 64, 256]
+    assert mod.cpu_thread_points({"affinity": 8, "quota_cores": None}) == [8]
+    assert mod.cpu_thread_points({"affinity": 8, "quota_cores": 16.0}) == [8]
+    assert mod.cpu_thread_points({"affinity": 128, "quota_cores": 2.5}) == [3, 6, 64, 128]
+
+
+def test_metric_names_the_chunk():
+    mod = _bench_module()
+    assert mod.chunk_name(65536) == "64 KiB" and mod.chunk_name(1 << 20) == "1 MiB"
+    assert mod.chunk_name(1024) == "1 KiB" and mod.chunk_name(4404020) == "4404020 B"

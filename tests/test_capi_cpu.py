@@ -225,3 +225,19 @@ def test_device_api_rejects_mismatched_shapes():
         encode_update_batch(c, 0, st[:, 0], st[:, 1], st[:, 4:], torch.zeros((8, 2, 64), dtype=torch.uint8))
     with pytest.raises(ValueError, match="apply_batch"):
         apply_batch(np.ones((1, 2), np.uint8), [st[:, 0], st[:2, 1]], [st[:, 4]])
+    # the hashed and padded encodes: parity with fewer stripes, rows or bytes, data of another k
+    from elect_amd.batch import encode_batch_hashed, encode_batch_padded, encode_batch_tiled
+    h = torch.zeros((16, 2), dtype=torch.int32)
+    lens = torch.zeros((16, 4), dtype=torch.int32)
+    for bad in (torch.zeros((8, 2, 64), dtype=torch.uint8), st[:, 4:5], st[:, 4:, :32]):
+        with pytest.raises(ValueError, match="parity"):
+            encode_batch_hashed(c, st[:, :4], bad, h)
+        with pytest.raises(ValueError, match="parity"):
+            encode_batch_padded(c, st[:, :4], lens, bad)
+    with pytest.raises(ValueError, match="data"):
+        encode_batch_hashed(c, st[:, :3], st[:, 4:], h)
+    with pytest.raises(ValueError, match="data"):
+        encode_batch_padded(c, st[:, :5], lens, st[:, 4:])
+    # a tiled view with a zero tile length: ValueError, not ZeroDivisionError
+    with pytest.raises(ValueError, match="tile"):
+        encode_batch_tiled(c, st[:, :4, :0], st[:, 4:, :0], 64)

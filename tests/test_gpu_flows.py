@@ -105,10 +105,12 @@ def test_encode_update_batch_ex(dev, oracle, k, m, L, padded, hashed, in_place):
                 assert int(got_h[s, r]) == oracle.java_hashcode(want[r]), (s, r)
 
 
-def test_tiled_update_hash_needs_m_le_8(dev):
-    """A hashed update of an m >= 9 code runs on the byte-granular kernel
-    (tests/test_gpu_parity.py::test_hashed_update_of_wide_codes), which has no
-    tiled form: the tiled call refuses it; untiled and unhashed tiled calls run."""
+def test_tiled_update_needs_m_le_8(dev):
+    """An update of an m >= 9 code is a 2 + m > 10 column product, wider than the
+    padded vector kernels that tiled launches ride on: the tiled call refuses it,
+    hashed or not, whether its units span one tile or several (up front, not in
+    the launcher); the untiled hashed call runs (the byte-granular kernel,
+    tests/test_gpu_parity.py::test_hashed_update_of_wide_codes)."""
     from elect_amd import _lib
     from elect_amd.batch import encode_update_batch_ex, encode_update_batch_tiled
     from elect_amd.coder import RSCoder
@@ -116,9 +118,14 @@ def test_tiled_update_hash_needs_m_le_8(dev):
     z = torch.zeros((B, L), dtype=torch.uint8, device=dev)
     p = torch.zeros((B, m, L), dtype=torch.uint8, device=dev)
     h = torch.zeros((B, m), dtype=torch.int32, device=dev)
-    with pytest.raises(_lib.ECInvalidArgument):
-        encode_update_batch_tiled(RSCoder(4, m), 0, z, z, p, p, L, hashes=h)
-    encode_update_batch_tiled(RSCoder(4, m), 0, z, z, p, p, L)
+    for chunk in (L, 3 * L):  # T = 1 and T = 3 tiles per unit (B = 2 stripes -> 2 / 6 tile rows)
+        T = chunk // L
+        zt = torch.zeros((B * T, L), dtype=torch.uint8, device=dev)
+        pt = torch.zeros((B * T, m, L), dtype=torch.uint8, device=dev)
+        with pytest.raises(_lib.ECInvalidArgument):
+            encode_update_batch_tiled(RSCoder(4, m), 0, zt, zt, pt, pt, chunk, hashes=h)
+        with pytest.raises(_lib.ECInvalidArgument):
+            encode_update_batch_tiled(RSCoder(4, m), 0, zt, zt, pt, pt, chunk)
     encode_update_batch_ex(RSCoder(4, m), 0, z, z, p, p, hashes=h)
     torch.cuda.synchronize()
     assert not p.any()  # all-zero units: zero parity, hash 31^L

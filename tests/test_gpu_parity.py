@@ -688,6 +688,47 @@ def test_hashed_update_of_wide_codes(dev, oracle, k, m):
         assert hs[r] == int(gh[s, r])
 
 
+@pytest.mark.parametrize("hashed", [False, True])
+def test_host_update_of_wide_code_above_tile(dev, oracle, hashed):
+    """The host path's batcher stores units above 64 KiB as tiles, but a tiled
+    launch needs the padded vector kernels (at most 10 columns): the (2+m)-column
+    update of an m = 9 code at ELECT's codeLength (4,404,020 B) must run untiled
+    instead of failing its batch.  Two concurrent callers (so the batch is shared);
+    against the oracle, bytes and hashCode()."""
+    import threading
+    from elect_amd.coder import RSCoder
+    k, m, L, t = 3, 9, 4404020, 1
+    coder = RSCoder(k, m)
+    enc = oracle.Encoder(k, m)
+    calls = []
+    for c in range(2):
+        rng = np.random.default_rng(90 + c)
+        old, new = rng.integers(0, 256, L, dtype=np.uint8), rng.integers(0, 256, L, dtype=np.uint8)
+        pin = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(m)]
+        lens = [L - 1000 * (c + 1), L - 77 * c]
+        calls.append((old, new, pin, lens, [np.zeros(L, np.uint8) for _ in range(m)], [None]))
+
+    def run(c):
+        torch.cuda.set_device(dev)
+        old, new, pin, lens, outs, res = calls[c]
+        ins = [old, new] + pin
+        res[0] = coder.encode_update_ex_host([x.ctypes.data for x in ins], t, [x.ctypes.data for x in outs], L,
+                                             old_new_lengths=lens, hashed=hashed)
+    th = [threading.Thread(target=run, args=(c,)) for c in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    for old, new, pin, lens, outs, res in calls:
+        o = np.where(np.arange(L) < lens[0], old, 0).astype(np.uint8)
+        n = np.where(np.arange(L) < lens[1], new, 0).astype(np.uint8)
+        want = enc.encode_update([o, n] + pin, t)
+        for r in range(m):
+            assert np.array_equal(outs[r], want[r]), r
+            if hashed:
+                assert res[0][r] == oracle.java_hashcode(want[r]), r
+
+
 @pytest.mark.parametrize("k,m", [(4, 2), (3, 5)])
 def test_encode_decode_batches_equal_per_batch_calls(dev, oracle, k, m):
     """elect_ec_encode_batches / _decode_batches (several chunk sizes, one call):

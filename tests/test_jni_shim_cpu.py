@@ -53,17 +53,22 @@ def _coding_matrix(buf, n1, n2):
     return "".join("".join(f" {buf[j + i * n1]}" for j in range(n1)) + "\n" for i in range(n2)) + "\n"
 
 
+def _decode_lines(k, m, era, L):
+    """decodeImpl's three lines, printed on every call (EC/NativeRSDecoder.c:57, 65, 68)."""
+    return ("NativeRSDecoder_decodeImpl, start to process: data unit = %d, parity unit = %d, data block size = %d\n"
+            % (k, m, L) +
+            "NativeRSDecoder_decodeImpl, read data: target recovery data block number = %d, the first recovery "
+            "request block ID = %d\n" % (len(era), era[0]) +
+            "NativeRSDecoder_decodeImpl, start do decode\n")
+
+
 def _decoder_block(oracle, k, m, dec, era, L):
     n = k + m
     em = oracle.cauchy_matrix(k, m).reshape(-1)
     rows = np.stack([oracle.cauchy_matrix(k, m)[i] for i in dec])
     _, inv = oracle.invert_matrix(rows)
     _, dm = oracle.decode_matrix(k, m, dec, era, False)
-    return ("NativeRSDecoder_decodeImpl, start to process: data unit = %d, parity unit = %d, data block size = %d\n"
-            % (k, m, L) +
-            "NativeRSDecoder_decodeImpl, read data: target recovery data block number = %d, the first recovery "
-            "request block ID = %d\n" % (len(era), era[0]) +
-            "NativeRSDecoder_decodeImpl, start do decode\n" +
+    return (_decode_lines(k, m, era, L) +
             "Recovering (numAllUnits = %d, numDataUnits = %d, numErased = %d)\n" % (n, k, len(era)) +
             " - ErasedIndexes = " + "".join(f" {e}" for e in era) +
             "       - DecodeIndex = " + "".join(f" {d}" for d in dec) +
@@ -72,25 +77,41 @@ def _decoder_block(oracle, k, m, dec, era, L):
             "DecodeMatrix:\n" + _coding_matrix(dm.reshape(-1), k, n))
 
 
-def test_verbose_dumps_match_reference_format(oracle):
-    """allowVerboseDump() == true: the shim prints EC/dump.c's dumpEncoder
-    (:61-73) and dumpDecoder (:75-104) blocks, after decodeImpl's three lines
-    (EC/NativeRSDecoder.c:57, 65, 68), with the oracle's matrices: the Cauchy
-    generator, gf_invert_matrix's (partial, when singular) inverse in a zeroed
-    MMAX x KMAX array, and the compat decode rows."""
+def _dump_cases(drv, lib, **env):
+    import os
     import re
-    lib, drv = build()
-    r = subprocess.run([drv, lib, "dump"], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([drv, lib, "dump"], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, **env))
     assert r.returncode == 0, r.stdout + r.stderr
-    cases = dict(re.findall(r"=== (.*?)\n(.*?)(?==== )", r.stdout, flags=re.S))
-    em = oracle.cauchy_matrix(4, 2).reshape(-1)
-    assert cases["encode RS(6,4)"] == ("Encoding (numAllUnits = 6, numParityUnits = 2, numDataUnits = 4)\n"
-                                       "\n\nEncodeMatrix:\n" + _coding_matrix(em, 4, 6))
+    return dict(re.findall(r"=== (.*?)\n(.*?)(?==== )", r.stdout, flags=re.S))
+
+
+def test_stdout_matches_libec(oracle):
+    """Standard output at the JNI boundary is libec.so's, verbose or not:
+    decodeImpl prints its three lines on every call (EC/NativeRSDecoder.c:57,
+    65, 68) and, with allowVerboseDump() true, EC/dump.c's dumpDecoder block
+    (:75-104, from processErasures, EC/erasure_coder.c:195-197) with the oracle's
+    matrices: the Cauchy generator, gf_invert_matrix's (partial, when singular)
+    inverse in a zeroed MMAX x KMAX array, and the compat decode rows.  encode and
+    encodeUpdate print nothing, verbose or not: libec.so's only dumpEncoder call
+    runs right after initCoder zeroes verbose (EC/erasure_coder.c:27, 61-63).
+    ELECT_EC_JNI_QUIET=1 silences the decode lines (an opt-out; the default is
+    the reference's)."""
+    lib, drv = build()
+    cases = _dump_cases(drv, lib)
+    assert cases["encode RS(6,4)"] == ""
+    assert cases["encodeUpdate RS(6,4)"] == ""
+    assert cases["quiet encode RS(6,4)"] == ""
     assert cases["decode RS(6,4) {4,1,2,3} erase {0}"] == _decoder_block(oracle, 4, 2, [4, 1, 2, 3], [0], 16)
     assert cases["decode RS(6,4) singular {1,1,2,3} erase {0,5}"] == \
         _decoder_block(oracle, 4, 2, [1, 1, 2, 3], [0, 5], 16)
     assert cases["decode RS(12,8) {2..8,10} erase {9,0}"] == \
         _decoder_block(oracle, 8, 4, [2, 3, 4, 5, 6, 7, 8, 10], [9, 0], 16)
+    assert cases["quiet decode RS(6,4) {4,1,2,3} erase {0}"] == _decode_lines(4, 2, [0], 16)
+    silenced = _dump_cases(drv, lib, ELECT_EC_JNI_QUIET="1")
+    assert silenced["quiet decode RS(6,4) {4,1,2,3} erase {0}"] == ""
+    assert silenced["decode RS(6,4) {4,1,2,3} erase {0}"] == \
+        _decoder_block(oracle, 4, 2, [4, 1, 2, 3], [0], 16)[len(_decode_lines(4, 2, [0], 16)):]
 
 
 def test_mock_jni_table_is_the_specification_layout():

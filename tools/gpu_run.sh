@@ -9,7 +9,7 @@ rm -f gpurun_out/*.log gpurun_out/status.txt  # no stale logs from an earlier ca
 export PYTHONUNBUFFERED=1
 export TMPDIR=/tmp
 OUT="$PWD/gpurun_out"
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
 run() {  # name seconds cmd...
     local name=$1 t=$2; shift 2
     echo "[$(date +%T)] start $name" | tee -a gpurun_out/status.txt
@@ -162,6 +162,14 @@ for step in "$@"; do
             run "bench_tiles_${tag}_mixed_$i" 300 python bench.py --config mixed $v || exit $?
             run "bench_tiles_${tag}_rs12_$i" 300 python bench.py --config rs12 $v || exit $?
         done; done ;;
+    rs12gap)  # RS(12,8) decode inside the headline line vs its own --config run, interleaved
+        for i in 1 2; do
+            run "rs12gap_alone20_$i" 300 python bench.py --config rs12 --steps 20 --warmup 3 || exit $?
+            run "rs12gap_inline_$i" 300 python bench.py --no-cpu --no-host --steps 20 || exit $?
+            run "rs12gap_inline_nosizes_$i" 300 python bench.py --no-cpu --no-host --no-sizes --steps 20 || exit $?
+            run "rs12gap_inline_first_$i" 300 python bench.py --no-cpu --no-host --no-sizes --steps 20 --configs-order rs12,mixed || exit $?
+            run "rs12gap_alone50_$i" 300 python bench.py --config rs12 || exit $?
+        done ;;
     padfill)  # padded encode vs content fill: where the time goes
         for f in 1.0 0.0 0.5 random; do
             run "bench_padded_fill_$f" 300 python bench.py --config padded --pad-fill $f || exit $?
