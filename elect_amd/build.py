@@ -25,8 +25,21 @@ LIB = os.path.join(HERE, "libelect_ec.so")
 STAMP = LIB + ".buildid"
 ARCH = os.environ.get("ELECT_EC_ARCH", "gfx950")
 
-SOURCES = ["ec_capi.cpp", "host_path.cpp", "rs_kernels.hip"]
-HEADERS = ["gf256.hpp", "rs_kernels.hpp", "host_path.hpp"]
+SOURCES = ["ec_capi.cpp", "host_path.cpp", "rs_kernels.hip", "rs_inst.hip"]
+HEADERS = ["gf256.hpp", "rs_kernels.hpp", "rs_impl.hpp", "host_path.hpp"]
+INST_KS = range(1, 17)  # rs_inst.hip, once per source-column count (ELECT_EC_INST_K)
+
+
+def units():
+    """(source, object stem, extra flags) of every translation unit: rs_inst.hip
+    once per K, so the kernel instances compile in parallel."""
+    out = []
+    for src in SOURCES:
+        if src == "rs_inst.hip":
+            out += [(src, f"rs_inst_k{k}", [f"-DELECT_EC_INST_K={k}"]) for k in INST_KS]
+        else:
+            out.append((src, os.path.splitext(src)[0], []))
+    return out
 FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"]
 
 
@@ -72,18 +85,20 @@ def build(force: bool = False, verbose: bool = False) -> str:
     bid = build_id()
     common = [*FLAGS, "-I", os.path.join(ROOT, "include"), f'-DELECT_EC_BUILD_ID="{bid}"']
 
-    def compile_one(src):
-        obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
-        cmd = [hipcc, *common, "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
+    def compile_one(unit):
+        src, stem, extra = unit
+        obj = os.path.join(BUILD, stem + ".o")
+        cmd = [hipcc, *common, *extra, "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
-            raise RuntimeError(f"compile failed: {src}\n{r.stderr}")
+            raise RuntimeError(f"compile failed: {src} {' '.join(extra)}\n{r.stderr}")
         return obj
 
-    with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
-        objs = list(ex.map(compile_one, SOURCES))
+    jobs = max(1, min(16, os.cpu_count() or 1))
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_one, units()))
     tmp = LIB + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)

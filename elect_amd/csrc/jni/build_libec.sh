@@ -18,6 +18,14 @@ gcc -O2 -fPIC -Wall -c -I"$JAVA_HOME/include" -I"$JAVA_HOME/include/linux" -I"$R
     "$ROOT/elect_amd/csrc/host_path.cpp" -o "$OUT/host_path.o"
 "$HIPCC" --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/include" -x hip -c \
     "$ROOT/elect_amd/csrc/rs_kernels.hip" -o "$OUT/rs_kernels.o"
+INST=""
+for k in $(seq 1 16); do  # the kernel instances, once per source-column count
+    "$HIPCC" --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/include" -DELECT_EC_INST_K=$k -x hip -c \
+        "$ROOT/elect_amd/csrc/rs_inst.hip" -o "$OUT/rs_inst_k$k.o" &
+    INST="$INST $OUT/rs_inst_k$k.o"
+    [ $((k % 8)) -eq 0 ] && wait
+done
+wait
 "$HIPCC" --offload-arch=gfx950 -shared -fPIC -o "$OUT/libec.so" \
-    "$OUT/libec_jni.o" "$OUT/ec_capi.o" "$OUT/host_path.o" "$OUT/rs_kernels.o"
+    "$OUT/libec_jni.o" "$OUT/ec_capi.o" "$OUT/host_path.o" "$OUT/rs_kernels.o" $INST
 echo "built $OUT/libec.so — copy it to \$CASSANDRA_HOME/lib/sigar-bin (README.md:60)"

@@ -7,11 +7,18 @@ name=$1; shift
 mkdir -p elect_amd/_ab
 python -m elect_amd.build >/dev/null
 H=/opt/rocm/bin/hipcc
+C="$H --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I include"
+objs=""
 for f in rs_kernels.hip host_path.cpp; do
-    $H --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I include "$@" -x hip -c elect_amd/csrc/$f -o elect_amd/_ab/${f%.*}_$name.o &
+    $C "$@" -x hip -c elect_amd/csrc/$f -o elect_amd/_ab/${f%.*}_$name.o &
+    objs="$objs elect_amd/_ab/${f%.*}_$name.o"
+done
+for k in $(seq 1 16); do  # rs_inst.hip once per source-column count, 8 at a time
+    $C "$@" -DELECT_EC_INST_K=$k -x hip -c elect_amd/csrc/rs_inst.hip -o elect_amd/_ab/rs_inst_k${k}_$name.o &
+    objs="$objs elect_amd/_ab/rs_inst_k${k}_$name.o"
+    [ $((k % 8)) -eq 0 ] && wait
 done
 wait
-$H --offload-arch=gfx950 -shared -fPIC -o elect_amd/_ab/libelect_ec_$name.so elect_amd/_build/ec_capi.o \
-    elect_amd/_ab/host_path_$name.o elect_amd/_ab/rs_kernels_$name.o
-rm elect_amd/_ab/rs_kernels_$name.o elect_amd/_ab/host_path_$name.o
+$H --offload-arch=gfx950 -shared -fPIC -o elect_amd/_ab/libelect_ec_$name.so elect_amd/_build/ec_capi.o $objs
+rm $objs
 echo elect_amd/_ab/libelect_ec_$name.so

@@ -18,11 +18,19 @@ fi
 case "${1:-build}" in
 build)
     mkdir -p $OUT
+    C="$H --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -I include $SAN"
+    objs=""
     for f in ec_capi.cpp host_path.cpp rs_kernels.hip; do
-        $H --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -I include $SAN -x hip -c elect_amd/csrc/$f -o $OUT/${f%.*}.o &
+        $C -x hip -c elect_amd/csrc/$f -o $OUT/${f%.*}.o &
+        objs="$objs $OUT/${f%.*}.o"
+    done
+    for k in $(seq 1 16); do  # rs_inst.hip once per source-column count
+        $C -DELECT_EC_INST_K=$k -x hip -c elect_amd/csrc/rs_inst.hip -o $OUT/rs_inst_k$k.o &
+        objs="$objs $OUT/rs_inst_k$k.o"
+        [ $((k % 8)) -eq 0 ] && wait
     done
     wait
-    $H --offload-arch=gfx950 -shared -fPIC $SAN -o $OUT/libelect_ec_san.so $OUT/ec_capi.o $OUT/host_path.o $OUT/rs_kernels.o
+    $H --offload-arch=gfx950 -shared -fPIC $SAN -o $OUT/libelect_ec_san.so $objs
     $H --offload-arch=gfx950 -O1 -g -std=c++17 -I include $SAN -x hip tools/sanitize/host_stress.cpp -o $OUT/host_stress \
         -L $OUT -lelect_ec_san -Wl,-rpath,'$ORIGIN' -pthread
     rm -f $OUT/*.o
