@@ -73,6 +73,12 @@ def parse():
     ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (PCIe) measurement")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the mixed (configs[3]) and RS(12,8) (configs[4]) lines of the headline run")
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="run the step untimed for this long before the --warmup steps, so the timed steps see "
+                         "the GPU's steady clocks (per-step series: decode runs ~4 points slow for the first "
+                         "~20 ms of load, DESIGN.md §5); 0 = off")
+    ap.add_argument("--per-step", action="store_true",
+                    help="headline: also print every timed step's encode and decode kernel times (diagnostics)")
     ap.add_argument("--configs-order", default="mixed,rs12",
                     help="headline: the BASELINE configs run after the headline phases, in this order")
     ap.add_argument("--no-sizes", action="store_true",
@@ -109,6 +115,10 @@ def parse():
                          "for all classes each, the default) or one call per class (0)")
     ap.add_argument("--mixed-streams", type=int, default=1,
                     help="mixed: issue the size classes on this many streams (1: one stream, in order)")
+    ap.add_argument("--mixed-lanes", type=int, default=1,
+                    help="mixed: keep this many disjoint copies of the batch and issue step i's grouped encode + "
+                         "decode (copy i %% S) on stream i %% S, so one step's launch tail overlaps the next "
+                         "step's ramp-up (independent stripes; 1 = one copy, one stream)")
     ap.add_argument("--mixed-share", type=int, default=0,
                     help="mixed: code rank 0's share of an N-rank partition on this GPU (strong-scaling probe)")
     ap.add_argument("--streams", type=int, default=1,
@@ -385,7 +395,7 @@ def size_sweep(args, world, rank, dev, coder, sizes=(1024, 1 << 20)):
             e[2].record()
             evs.append(e)
 
-        dt, submit = timed(step, args.steps, args.warmup, world)
+        dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms)
         enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs[-args.steps:]) / args.steps
         dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs[-args.steps:]) / args.steps
         res[str(L)] = {
@@ -464,14 +474,29 @@ def alloc_stripes(args, B: int, L: int, k: int, m: int, dev, generator=None):
     return st, Bc, Lc
 
 
-def timed(step, steps, warmup, world):
+def settle(step, ms: float) -> int:
+    """Run `step` untimed for about `ms` of wall time (synchronising every few
+    steps so the host does not run ahead); returns the steps run."""
+    n, t0 = 0, time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        step()
+        n += 1
+        if n % 8 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    return n
+
+
+def timed(step, steps, warmup, world, settle_ms: float = 0.0):
     """Warm up, then time exactly `steps` steps between barrier + synchronize on
     both sides.  Each rank's clock starts when the opening barrier releases it
     and stops at its closing synchronize (the closing gloo barrier costs ~0.6 ms
     at 8 ranks, a few % of a 20-step region, and is no part of a step); the
     max over ranks is the job's time.  Returns (max over ranks of the elapsed seconds, this rank's host
     submit time per step in ms: the time the host spends issuing one step's
-    launches, which must stay well below the step's GPU time)."""
+    launches, which must stay well below the step's GPU time).  settle_ms:
+    untimed steps before the warmup (settle())."""
+    settle(step, settle_ms)
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -524,12 +549,16 @@ def config_mixed(args, world, rank, dev):
     # each GPU of an N-GPU run does under strong scaling), to see the per-GPU rate there
     parts, prank = (args.mixed_share, 0) if args.mixed_share else (world, rank)
     share_bytes = 0
+    lanes = max(1, args.mixed_lanes)
+    copies = [[] for _ in range(lanes)]  # --mixed-lanes: disjoint copies of the classes, one per lane
     for L in (1024, 4096, 1 << 20):
         total = (1 << 30) // (k * L)
         b, e = partition_by_bytes([k * L] * total, parts, prank)
         share_bytes += 2 * (e - b) * k * L
-        st, Bc, Lc = alloc_stripes(args, e - b, L, k, m, dev)
-        classes.append((L, st, torch.empty((Bc, 1, Lc), dtype=torch.uint8, device=dev)))
+        for c in range(lanes):
+            st, Bc, Lc = alloc_stripes(args, e - b, L, k, m, dev)
+            copies[c].append((L, st, torch.empty((Bc, 1, Lc), dtype=torch.uint8, device=dev)))
+    classes = copies[0]
 
     # --mixed-streams S: the classes are independent batches; with S > 1 class i is issued on
     # stream i % S behind an event from the step's stream (and joined back at the end), so
@@ -537,12 +566,24 @@ def config_mixed(args, world, rank, dev):
     main = torch.cuda.current_stream()
     streams = [main] if args.mixed_streams <= 1 else [torch.cuda.Stream() for _ in range(args.mixed_streams)]
 
-    enc_pairs = [(st[:, :k], st[:, k:]) for _, st, _ in classes]
-    dec_pairs = [(st, out) for _, st, out in classes]
+    torch.cuda.synchronize()  # the copies' contents are written before any lane reads them
+    enc_pairs = [[(st[:, :k], st[:, k:]) for _, st, _ in cl] for cl in copies]
+    dec_pairs = [[(st, out) for _, st, out in cl] for cl in copies]
+    lane_streams = [torch.cuda.Stream() for _ in range(lanes)] if lanes > 1 else None
+    turn = [0]
 
     def step_grouped():  # elect_ec_encode_batches / _decode_batches: one launch for all classes each
-        encode_batches(coder, enc_pairs)
-        decode_batches(coder, dec_pairs, [1, 2, 3, 4], [0], inputs_by_unit=True)
+        c = turn[0] % lanes
+        turn[0] += 1
+        if lane_streams is None:
+            encode_batches(coder, enc_pairs[0])
+            decode_batches(coder, dec_pairs[0], [1, 2, 3, 4], [0], inputs_by_unit=True)
+            return
+        # copy c only ever runs on lane c, so its steps stay ordered; timed() synchronises
+        # the whole device around the timed region
+        with torch.cuda.stream(lane_streams[c]):
+            encode_batches(coder, enc_pairs[c])
+            decode_batches(coder, dec_pairs[c], [1, 2, 3, 4], [0], inputs_by_unit=True)
 
     def step():
         if args.mixed_group:
@@ -564,8 +605,8 @@ def config_mixed(args, world, rank, dev):
                 cur.wait_event(done)
 
     run = graph_steps([step])[0] if args.graph else step
-    dt, submit = timed(run, args.steps, args.warmup, world)
-    ok = all(torch.equal(out[:, 0], st[:, 0]) for _, st, out in classes)
+    dt, submit = timed(run, args.steps, args.warmup, world, args.settle_ms)
+    ok = all(torch.equal(out[:, 0], st[:, 0]) for cl in copies for _, st, out in cl)
     data = 2 * 3 * (1 << 30)  # enc + dec, 3 classes, all ranks together
     per_class = {}  # outside the timed region: each class's kernels by HIP events (median of 9)
     for L, st, out in classes:
@@ -625,7 +666,7 @@ def config_rs12(args, world, rank, dev):
         e1.record()
         evs.append((e0, e1))
 
-    dt, submit = timed(step, args.steps, args.warmup, world)
+    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms)
     ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
     ok = torch.equal(out, st[:, :2])
     alg = B * (k + 2) * L
@@ -656,6 +697,7 @@ def config_rs12(args, world, rank, dev):
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                          "kernel": "gf_apply_x16<8,2> (decode)", "algorithmic_bytes_per_launch": alg},
+            **({"per_step_ms": [round(a.elapsed_time(b), 4) for a, b in evs[-args.steps:]]} if args.per_step else {}),
             "config": {"workload": f"RS(12,8) decode erase {{0,1}} from {surv}, {B} x {L} B stripes per GPU",
                        "layout": LAYOUT_NAMES[layout_for(args, L)],
                        "parallelism": f"stripe-partitioned x{world}"}}
@@ -820,7 +862,7 @@ def config_update(args, world, rank, dev):
         e1.record()
         evs.append((e0, e1))
 
-    dt, submit = timed(step, args.steps, args.warmup, world)
+    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms)
     ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
     # self-check through the product: updating twice with the same delta restores the parity
     ref = par.clone()
@@ -863,7 +905,7 @@ def config_padded(args, world, rank, dev):
         e1.record()
         evs.append((e0, e1))
 
-    dt, submit = timed(step, args.steps, args.warmup, world)
+    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms)
     ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
     # self-check through the product: explicit zero fill + plain encode gives the same parity
     idx = torch.arange(L, device=dev).view(1, 1, L)
@@ -908,7 +950,7 @@ def config_hashed(args, world, rank, dev):
         e1.record()
         evs.append((e0, e1))
 
-    dt, submit = timed(step, args.steps, args.warmup, world)
+    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms)
     ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
     ref = torch.empty_like(par)
     encode_batch(coder, data, ref)
@@ -1035,7 +1077,7 @@ def config_flows(args, world, rank, dev):
         for i, nm in enumerate(("encode", "update", "decode")):
             ev[nm].append((es[i], es[i + 1]))
 
-    dt, submit = timed(step, args.steps, args.warmup, world)
+    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms)
     ms = {nm: sum(a.elapsed_time(b) for a, b in v[-args.steps:]) / args.steps for nm, v in ev.items()}
     # self-check through the product (coded untiled, contiguous): the new parity is the
     # encode of the zero-filled stripe with unit t replaced, its hashes match, and the
@@ -1227,6 +1269,7 @@ def main():
         if ev is not None:
             ev[2].record(stream)
 
+    settle_steps = settle(step, args.settle_ms)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -1254,6 +1297,8 @@ def main():
         replays = keep
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    per_step = {"encode": [round(e[0].elapsed_time(e[1]), 4) for e in evs],
+                "decode": [round(e[1].elapsed_time(e[2]), 4) for e in evs]} if args.per_step else None
     if args.decode_out == "inplace":  # unit 0 was rebuilt in place: it must still be the original data
         ok = bool(torch.equal(stripe[:, 0], orig0))
     else:
@@ -1289,6 +1334,7 @@ def main():
             "parallelism": f"stripe-partitioned x{world}, no collectives (gloo timing handshake only)",
             "graph": bool(args.graph),
             "streams": args.streams,
+            "settle": {"ms": args.settle_ms, "steps": settle_steps},  # untimed, before the warmup steps
         },
         "host_submit_ms_per_step": round(submit_ms, 4),
         "roofline": {
@@ -1312,6 +1358,8 @@ def main():
         },
         "verified": ok,
     }
+    if per_step:
+        out["per_step_ms"] = per_step
     rec = {"rank": rank, "device": local, "ms_per_step": round(own / args.steps * 1e3, 4),
            "host_submit_ms_per_step": round(submit_ms, 4), "encode_frac": out["kernels"]["encode"]["frac"],
            "decode_frac": out["kernels"]["decode_1erasure"]["frac"], "verified": ok}

@@ -162,6 +162,33 @@ for step in "$@"; do
             run "bench_tiles_${tag}_mixed_$i" 300 python bench.py --config mixed $v || exit $?
             run "bench_tiles_${tag}_rs12_$i" 300 python bench.py --config rs12 $v || exit $?
         done; done ;;
+    perstep)  # every step's kernel times from a cold start: is the in-line shortfall a warm-up transient?
+        run perstep_head200 300 python bench.py --no-cpu --no-host --no-sizes --no-configs --warmup 0 --steps 200 --per-step || exit $?
+        run perstep_head20 300 python bench.py --no-cpu --no-host --no-sizes --no-configs --warmup 5 --steps 20 --per-step || exit $?
+        run perstep_rs12 300 python bench.py --config rs12 --warmup 0 --steps 200 --per-step || exit $?
+        run perstep_head_inline 300 python bench.py --no-cpu --no-host --no-sizes --warmup 5 --steps 20 --per-step || exit $? ;;
+    settle)  # the driver's shape (--steps 20 --warmup 5) with and without the settle phase, interleaved
+        for i in 1 2 3; do for sm in 100 0; do
+            run "settle${sm}_$i" 300 python bench.py --no-cpu --no-host --steps 20 --warmup 5 --settle-ms $sm --per-step || exit $?
+        done; done ;;
+    mixedlanes)  # the mixed config's 8-way share (and full size): lanes (copies x streams) 1 / 2, interleaved
+        for i in 1 2 3; do for ln in 1 2; do for sh in 8 0; do
+            run "mixedlanes_l${ln}_s${sh}_$i" 300 python bench.py --config mixed --mixed-share $sh --mixed-lanes $ln --steps 50 || exit $?
+        done; done; done ;;
+    mixedprof)  # kernel trace of the 8-way share: kernel durations against the step (gaps, ramp)
+        run mixedprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/mixedprof_$TAG -o run \
+            -- python3 bench.py --config mixed --mixed-share 8 --steps 50 --settle-ms 0 || exit $? ;;
+    rs12pmc)  # RS(12,8) decode alone vs after the mixed config: DRAM credit stalls, bytes, effective clock
+        PA="GRBM_GUI_ACTIVE TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum"
+        for v in alone inline; do
+            args="--config rs12 --steps 20 --warmup 3"
+            [ $v = inline ] && args="--no-cpu --no-host --no-sizes --no-hostpath --steps 20 --configs-order mixed,rs12"
+            for pass in A F W; do
+                ctr=$PA; [ $pass = F ] && ctr="FETCH_SIZE GRBM_GUI_ACTIVE"; [ $pass = W ] && ctr="WRITE_SIZE GRBM_GUI_ACTIVE"
+                run "rs12pmc_${v}_$pass" 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/rs12pmc_${v}_$pass -o run \
+                    -- python3 bench.py $args || exit $?
+            done
+        done ;;
     rs12gap)  # RS(12,8) decode inside the headline line vs its own --config run, interleaved
         for i in 1 2; do
             run "rs12gap_alone20_$i" 300 python bench.py --config rs12 --steps 20 --warmup 3 || exit $?
