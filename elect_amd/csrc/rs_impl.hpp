@@ -40,6 +40,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -856,6 +857,103 @@ __global__ __launch_bounds__(kBlock) void gf_apply_group(const GroupArgs<K, R> a
     for (int r = 0; r < R; ++r) store_nt(g.dp[r] + stripe * g.ds[r] + off, acc[r]);
 }
 
+// Plain launches with U segments per lane (A/B: AB_PLAIN_U > 1): a wave codes
+// U adjacent 1 KiB slices per column, all U*K loads issued before any compute,
+// so a wave keeps U times the bytes in flight at the same occupancy cap.
+template <int K, int R, int U>
+__global__ __launch_bounds__(kBlock) void gf_apply_x16m(const FastArgs<K, R> a)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t first = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * (64u * U);
+    stage_tables<K, R>(a.tab, tl);
+    if (__builtin_amdgcn_readfirstlane(first) >= a.total) return;
+    uint4 x[U][K];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t idx = min(first + u * 64u + lane, a.total - 1);  // past the end: redo the last segment
+        const uint32_t stripe = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
+        const uint64_t off = static_cast<uint64_t>(idx - stripe * a.segs) * 16;
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[u][j] = load_nt(a.sp[j] + stripe * a.ss[j] + off);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t idx = first + u * 64u + lane;
+        if (idx >= a.total) break;
+        const uint32_t stripe = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
+        const uint64_t off = static_cast<uint64_t>(idx - stripe * a.segs) * 16;
+        uint4 acc[R];
+        gf_combine<K, R>(x[u], tl, acc);
+#pragma unroll
+        for (int r = 0; r < R; ++r) store_nt(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent forms of the plain and grouped kernels: one resident wave of
+// workgroups (grid = CUs x the blocks the occupancy cap lets each CU hold),
+// each staging the tables ONCE and then walking the launch's blocks in a
+// grid stride (virtual block b = blockIdx.x, + gridDim.x, ...).  Every
+// virtual block codes exactly the segments the ordinary launch's block b
+// would, so bytes, order of HBM windows and results are unchanged; what goes
+// is the per-block wave launch and table staging (kernarg loads, LDS writes,
+// a barrier) on the critical path of every 1 KiB per column.  No block waits
+// on another: each loop ends when its next virtual block is past the launch.
+// ---------------------------------------------------------------------------
+template <int K, int R, bool UNI>
+__global__ __launch_bounds__(kBlock) void gf_apply_x16p(const FastArgs<K, R> a, uint32_t vblocks)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
+    stage_tables<K, R>(a.tab, tl);
+    for (uint32_t b = blockIdx.x; b < vblocks; b += gridDim.x) {
+        const uint32_t idx = b * blockDim.x + threadIdx.x;
+        if (idx >= a.total) break;  // (UNI: whole waves; later blocks lie further past the end)
+        uint32_t stripe;
+        uint64_t off;
+        if constexpr (UNI) {
+            stripe = div_magic(__builtin_amdgcn_readfirstlane(idx), a.magic, a.shift);
+            off = static_cast<uint32_t>((idx - stripe * a.segs) * 16u);
+        } else {
+            stripe = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
+            off = static_cast<uint64_t>(idx - stripe * a.segs) * 16;
+        }
+        uint4 x[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + static_cast<uint64_t>(stripe) * a.ss[j] + off);
+        uint4 acc[R];
+        gf_combine<K, R>(x, tl, acc);
+#pragma unroll
+        for (int r = 0; r < R; ++r) store_nt(a.dp[r] + static_cast<uint64_t>(stripe) * a.ds[r] + off, acc[r]);
+    }
+}
+
+template <int K, int R, bool UNI>
+__global__ __launch_bounds__(kBlock) void gf_apply_groupp(const GroupArgs<K, R> a, uint32_t vblocks)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
+    stage_tables<K, R>(a.tab, tl);
+    for (uint32_t b = blockIdx.x; b < vblocks; b += gridDim.x) {
+        int p = 0;
+        for (int q = 1; q < a.n; ++q)
+            if (b >= a.part[q].block0) p = q;
+        const GroupPart<K, R>& g = a.part[p];
+        const uint32_t idx = (b - g.block0) * blockDim.x + threadIdx.x;
+        if (idx >= g.total) continue;  // the part's last block may be partial; later blocks are other parts
+        const uint32_t stripe = UNI ? div_magic(__builtin_amdgcn_readfirstlane(idx), g.magic, g.shift)
+                                    : static_cast<uint32_t>((static_cast<uint64_t>(idx) * g.magic) >> g.shift);
+        const uint64_t off = UNI ? static_cast<uint64_t>(static_cast<uint32_t>((idx - stripe * g.segs) * 16u))
+                                 : static_cast<uint64_t>(idx - stripe * g.segs) * 16;
+        uint4 x[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = load_nt(g.sp[j] + stripe * g.ss[j] + off);
+        uint4 acc[R];
+        gf_combine<K, R>(x, tl, acc);
+#pragma unroll
+        for (int r = 0; r < R; ++r) store_nt(g.dp[r] + stripe * g.ds[r] + off, acc[r]);
+    }
+}
+
 #ifndef AB_PAD_U4
 #define AB_PAD_U4 4
 #endif
@@ -926,6 +1024,18 @@ constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches ar
 #define AB_WAVES_WRITE_HEAVY 24
 #endif
 constexpr size_t kLdsPerCU = 160 * 1024;
+#ifndef AB_PERSIST
+#define AB_PERSIST 0
+#endif
+#ifndef AB_PLAIN_U  // A/B: segments per lane of plain (per-lane addressed) launches; 1 = gf_apply_x16
+#define AB_PLAIN_U 1
+#endif
+#ifndef AB_PLAIN_U_MAX_R  // ... for launches of at most this many output rows (1: decodes only)
+#define AB_PLAIN_U_MAX_R 4
+#endif
+#ifndef AB_PLAIN_U_WAVES  // ... and this occupancy cap (0: plain_waves_cap)
+#define AB_PLAIN_U_WAVES 0
+#endif
 
 inline int plain_waves_cap(int cols, int rows)
 {
@@ -951,6 +1061,40 @@ inline size_t cap_lds(int block, int coefs, int waves)
     const size_t static_lds = static_cast<size_t>(coefs) * kTabStride * sizeof(uint32_t);
     const size_t per_block = kLdsPerCU / blocks - 512;  // > kLdsPerCU / (blocks + 1): one block fewer fits
     return per_block > static_lds ? per_block - static_lds : 0;
+}
+
+// Persistent launches (gf_apply_x16p / gf_apply_groupp): ELECT_EC_PERSIST = 0
+// (off), 1 (plain and grouped launches) or 2 (grouped only); read once.
+inline int persist_mode()
+{
+    static const int m = [] {
+        const char* e = std::getenv("ELECT_EC_PERSIST");
+        return e ? std::atoi(e) : AB_PERSIST;
+    }();
+    return m;
+}
+
+// Compute units of the current device (cached per device).
+inline int device_cus()
+{
+    static std::mutex mu;
+    static int cus[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!cus[dev]) {
+        int n = 0;
+        cus[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+    }
+    return cus[dev];
+}
+
+// Grid of a persistent launch: every CU holds `waves` waves (the occupancy cap)
+// of `block`-thread blocks, at most the launch's own block count.
+inline uint32_t persist_grid(uint64_t vblocks, int block, int waves)
+{
+    const uint64_t per_cu = static_cast<uint64_t>(std::max(1, waves / (block / 64)));
+    return static_cast<uint32_t>(std::min<uint64_t>(vblocks, per_cu * static_cast<uint64_t>(device_cus())));
 }
 
 // Padded launches the per-stripe-length kernel can take (whole 16-byte segments,
@@ -1079,7 +1223,29 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             if constexpr (!PAD)
                 scalar_base = (a.hashes ? AB_SCALAR_BASE_HASH != 0 && K <= kMaxHashCols : kPlainU) &&
                               a.segs % 64 == 0 && segs64 < (uint64_t{1} << 28);
-            if (scalar_base) {
+            if (AB_PLAIN_U > 1 && !PAD && !a.hashes && !scalar_base && R <= AB_PLAIN_U_MAX_R) {  // A/B: U per lane
+                if constexpr (!PAD && AB_PLAIN_U > 1) {
+                    constexpr int U = AB_PLAIN_U;
+                    const uint64_t th = (static_cast<uint64_t>(a.total) + 64 * U - 1) / (64 * U) * 64;
+                    hipLaunchKernelGGL((gf_apply_x16m<K, R, U>), dim3(static_cast<uint32_t>((th + block - 1) / block)),
+                                       dim3(block), cap_lds(block, R * K, AB_PLAIN_U_WAVES ? AB_PLAIN_U_WAVES : plain_waves_cap(K, R)),
+                                       stream, a);
+                }
+            } else if (!PAD && !a.hashes && persist_mode() == 1) {  // persistent form (gf_apply_x16p)
+                if constexpr (!PAD) {
+                    const int waves = plain_waves_cap(K, R);
+                    const dim3 pg(persist_grid(grid, block, waves));
+                    const size_t lds = cap_lds(block, R * K, waves);
+                    if constexpr (kPlainU) {
+                        if (scalar_base)
+                            hipLaunchKernelGGL((gf_apply_x16p<K, R, true>), pg, dim3(block), lds, stream, a, grid);
+                        else
+                            hipLaunchKernelGGL((gf_apply_x16p<K, R, false>), pg, dim3(block), lds, stream, a, grid);
+                    } else {
+                        hipLaunchKernelGGL((gf_apply_x16p<K, R, false>), pg, dim3(block), lds, stream, a, grid);
+                    }
+                }
+            } else if (scalar_base) {
                 if constexpr (!PAD && kPlainU) {
                     if (!a.hashes)
                         hipLaunchKernelGGL((gf_apply_x16u<K, R, false>), dim3(grid), dim3(block),
@@ -1168,6 +1334,20 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
         blocks += (g.total + block - 1) / block;
     }
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    if (persist_mode() >= 1) {  // persistent form (gf_apply_groupp)
+        const int waves = plain_waves_cap(K, R);
+        const dim3 pg(persist_grid(blocks, block, waves));
+        const size_t lds = cap_lds(block, R * K, waves);
+        const uint32_t vb = static_cast<uint32_t>(blocks);
+        if constexpr (K >= AB_SCALAR_BASE_MIN_K) {
+            if (uni) {
+                hipLaunchKernelGGL((gf_apply_groupp<K, R, true>), pg, dim3(block), lds, stream, a, vb);
+                return hipGetLastError();
+            }
+        }
+        hipLaunchKernelGGL((gf_apply_groupp<K, R, false>), pg, dim3(block), lds, stream, a, vb);
+        return hipGetLastError();
+    }
     if constexpr (K >= AB_SCALAR_BASE_MIN_K) {
         if (uni) {
             hipLaunchKernelGGL((gf_apply_group<K, R, true>), dim3(static_cast<uint32_t>(blocks)), dim3(block),

@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-rm -f gpurun_out/*.log gpurun_out/status.txt  # no stale logs from an earlier call
+[ -n "${KEEP_LOGS:-}" ] || rm -f gpurun_out/*.log gpurun_out/status.txt  # no stale logs from an earlier call
 export PYTHONUNBUFFERED=1
 export TMPDIR=/tmp
 OUT="$PWD/gpurun_out"
@@ -189,6 +189,25 @@ for step in "$@"; do
                     -- python3 bench.py $args || exit $?
             done
         done ;;
+    padpmc)  # the padded per-stripe-length encode: HBM bytes against the content it needs, and its stalls
+        PA="GRBM_GUI_ACTIVE TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum"
+        for fill in random 1.0; do
+            run "padpmc_${fill}_bench" 120 python bench.py --config padded --pad-fill $fill --steps 20 || exit $?
+            for pass in A F W; do
+                ctr=$PA; [ $pass = F ] && ctr="FETCH_SIZE GRBM_GUI_ACTIVE"; [ $pass = W ] && ctr="WRITE_SIZE GRBM_GUI_ACTIVE"
+                run "padpmc_${fill}_$pass" 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/padpmc_${fill}_$pass -o run \
+                    -- python3 bench.py --config padded --pad-fill $fill --steps 20 || exit $?
+            done
+        done ;;
+    persist)  # persistent plain/grouped kernels (ELECT_EC_PERSIST): GPU suite under it, then interleaved A/B
+        ELECT_EC_PERSIST=1 run pytest_gpu_persist 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 || exit $?
+        for i in 1 2 3; do for P in 0 1; do
+            ELECT_EC_PERSIST=$P run "persist${P}_headline_$i" 300 python bench.py --no-cpu --no-host --no-configs --steps 50 || exit $?
+            ELECT_EC_PERSIST=$P run "persist${P}_mixed8_$i" 300 python bench.py --config mixed --mixed-share 8 --steps 50 || exit $?
+            ELECT_EC_PERSIST=$P run "persist${P}_mixed_$i" 300 python bench.py --config mixed --steps 50 || exit $?
+            ELECT_EC_PERSIST=$P run "persist${P}_rs12_$i" 300 python bench.py --config rs12 --steps 50 || exit $?
+        done; done ;;
+    zerocopy) run zerocopy 600 python tools/tune/zerocopy_probe.py || exit $? ;;
     rs12gap)  # RS(12,8) decode inside the headline line vs its own --config run, interleaved
         for i in 1 2; do
             run "rs12gap_alone20_$i" 300 python bench.py --config rs12 --steps 20 --warmup 3 || exit $?
