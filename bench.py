@@ -781,7 +781,7 @@ def config_hostpath(args, world, rank, dev):
         "encode"
     return {"metric": f"GiB/s host-memory RS(6,4) {op_name} through the C ABI (JNI calling convention)",
             "value": round(T * done * k * L / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
-            "devices": ndev, "callers": T,
+            "devices": ndev, "callers": T, "host_path_stats": _lib.host_path_stats(),
             "steps": done, "warmup": 1, "ms_per_step": round(dt / done * 1e3, 3), "higher_is_better": True,
             "scaling": "none", "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
             "config": {"workload": f"{T} threads x {done} synchronous elect_ec_{args.host_op} calls, one stripe "
@@ -837,6 +837,7 @@ def hostpath_all_devices(args, world, rank, child=None):
         else:
             o = json.loads(line)
             res = {"value": o["value"], "unit": o["unit"], "devices": o["devices"], "callers": o["callers"],
+                   "host_path_stats": o.get("host_path_stats"),
                    "calls_per_caller": o["steps"], "verified": bool(o["verified"]),
                    "workload": o["config"]["workload"], "parallelism": o["config"]["parallelism"]}
     barrier(world)

@@ -75,6 +75,7 @@ SIGNATURES = [
     ("elect_ec_unaligned_vector_ok", ctypes.c_int, [_ip]),
     ("elect_ec_set_host_devices", ctypes.c_int, [_ip, ctypes.c_int]),
     ("elect_ec_set_batching", ctypes.c_int, [ctypes.c_int, ctypes.c_uint, ctypes.c_size_t]),
+    ("elect_ec_host_path_stats", ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     ("elect_ec_coder_create", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_cp)]),
     ("elect_ec_coder_destroy", None, [_cp]),
     ("elect_ec_coder_num_data_units", ctypes.c_int, [_cp]),
@@ -193,6 +194,13 @@ def set_host_devices(devices) -> None:
 def set_batching(enable: bool, window_us: int = 0, arena_bytes: int = 256 << 20) -> None:
     """Cross-thread batching of concurrent host-memory encodes/decodes of one shape."""
     check(lib.elect_ec_set_batching(int(enable), window_us, arena_bytes), "set_batching")
+
+
+def host_path_stats() -> dict:
+    """The host-memory path's counters (elect_ec_host_path_stats)."""
+    out = (ctypes.c_uint64 * 4)()
+    lib.elect_ec_host_path_stats(out, 4)
+    return {"zero_copy": out[0], "zero_copy_fallback": out[1], "batched": out[2], "per_thread": out[3]}
 
 
 def ptr_array(addrs) -> ctypes.Array:

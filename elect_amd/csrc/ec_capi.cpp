@@ -290,6 +290,8 @@ int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes)
     return elect::host::set_batching(enable, window_us, arena_bytes);
 }
 
+int elect_ec_host_path_stats(uint64_t* out, int n) { return elect::host::host_path_stats(out, n); }
+
 int elect_ec_coder_create(int num_data_units, int num_parity_units, elect_ec_coder** out)
 {
     if (!out) return ELECT_EC_EINVAL;

@@ -52,6 +52,7 @@ struct HostOp {
 int run_host(const HostOp& op, size_t len);
 int set_host_devices(const int* devices, int n);
 int set_batching(int enable, unsigned window_us, size_t arena_bytes);
+int host_path_stats(uint64_t* out, int n);  // elect_ec_host_path_stats
 
 }  // namespace host
 }  // namespace elect

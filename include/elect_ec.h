@@ -106,6 +106,14 @@ int elect_ec_set_host_devices(const int* devices, int n);
  * at the per-thread path's rate (11.5-14 GiB/s). */
 int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes);
 
+/* Counters of the host-memory path since the process started, for diagnostics:
+ * out[0] zero-copy calls (a lone caller's buffers page-locked and coded in
+ * place over PCIe; ELECT_EC_ZEROCOPY=0 off, 1 default, 2 every eligible call),
+ * out[1] zero-copy attempts that fell back (registration refused), out[2]
+ * calls coded through the cross-thread batcher, out[3] calls coded by the
+ * per-thread staging engine.  Writes min(n, 4) entries; returns the count. */
+int elect_ec_host_path_stats(uint64_t* out, int n);
+
 /* ---- coder lifecycle ----
  * Replaces initEncoder / initDecoder (EC/erasure_coder.c:49-72) as called by
  * NativeRSEncoder_initImpl (EC/NativeRSEncoder.c:31-40) and NativeRSDecoder_initImpl
