@@ -924,7 +924,7 @@ def config_padded(args, world, rank, dev):
             "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "gf_apply_lens<4,2,4> (padded, per-stripe lengths)", "algorithmic_bytes_per_launch": alg,
+                         "kernel": "gf_apply_lens<4,2,2> (padded, per-stripe lengths)", "algorithmic_bytes_per_launch": alg,
                          "fill": round(valid / (B * k * L), 3)},
             "config": {"workload": f"{B} stripes, content lengths " + (f"uniform in [0, {L}]" if args.pad_fill == "random"
                                                                      else f"{args.pad_fill} x {L}"),

@@ -11,6 +11,7 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -844,23 +845,25 @@ Batcher* batcher(int dev)
 }
 
 // ---------------------------------------------------------------------------
-// Zero-copy calls.  A caller that finds at most one other host-path call in
-// flight on its device has its own buffers page-locked for the duration of the
-// call (hipHostRegister), and the kernel reads its units and writes its outputs
-// over PCIe directly: no staging copies, no DMA stages, no helper threads.
+// Zero-copy calls.  A caller that is alone on its device (no other call in
+// flight, no other thread calling for 20 ms: lone_caller) has its own buffers page-locked for the duration of the call
+// (hipHostRegister), and the kernel reads its units and writes its outputs over
+// PCIe directly: no staging copies, no DMA stages, no helper threads.
 // tools/tune/zerocopy_probe.py (RS(6,4), 4,404,020 B, one caller): 35.4 GiB/s
 // against 22.1 for the staged path (register 0.02 ms and unregister 0.01 ms per
-// call; kernel 0.43 ms).  Many concurrent callers lose with it (registration
-// contends in the driver: 7.8 + 12.6 ms per call at 64 callers, and 64 kernels
-// reading host memory at once run at 26 GiB/s against the batch's 44), so they
-// keep the batcher.  ELECT_EC_ZEROCOPY: 0 off, 1 (default) lone callers with
+// call; kernel 0.43 ms); through the product (bench.py --config hostpath, 2 s
+// runs, profiles/r03/zerocopy_hostpath.txt): 1 caller 31.9-32.2 against 22.6
+// GiB/s staged, but 2 callers 35.9 against 38.8-39.3 batched.  Concurrent
+// callers lose with it (registration contends in the driver: 7.8 + 12.6 ms per
+// call at 64 callers, and 64 kernels reading host memory at once run at 26
+// GiB/s against the batch's 44), so only a lone caller takes it.  ELECT_EC_ZEROCOPY: 0 off, 1 (default) lone callers with
 // units of at least kMinBytes, 2 every eligible call (tests).  Hashed calls keep
 // the staged path.  Any registration failure (memory already locked by another
 // call, a mapping the driver refuses) falls back to the staged path.
 // ---------------------------------------------------------------------------
 struct ZeroCopy {
     static constexpr size_t kMinBytes = size_t{1} << 20;  // mmap-backed buffers: no page shared with another caller
-    static constexpr int kMaxInFlight = 2;                // callers on the device, this one included
+    static constexpr int kMaxInFlight = 1;                // callers on the device, this one included
     static constexpr int kFallback = -1000;
 
     static int mode()
@@ -872,11 +875,11 @@ struct ZeroCopy {
         return m;
     }
 
-    static bool eligible(const HostOp& op, size_t len, int in_flight)
+    static bool eligible(const HostOp& op, size_t len, int in_flight, bool alone)
     {
         const int m = mode();
         if (m == 0 || op.hashes || len > 0xFFFFFFFFull) return false;
-        return m == 2 || (len >= kMinBytes && in_flight <= kMaxInFlight);
+        return m == 2 || (len >= kMinBytes && in_flight <= kMaxInFlight && alone);
     }
 
     // Page-aligned, merged [begin, end) intervals covering every unit of the call.
@@ -956,6 +959,23 @@ struct ZeroCopy {
 
 // Host-path calls in flight per device (run_host), for the zero-copy policy.
 std::atomic<int> g_in_flight[kMaxDevices];
+// The last calling thread per device, and when a different thread last called:
+// a caller is alone when no other thread has called for kAloneNs.  Two threads
+// calling back to back are each momentarily alone between calls, and a
+// zero-copy call then competes with the other's batched DMA (2 callers: 31.5-
+// 34.7 GiB/s against 36.0-36.2 batched, profiles/r03/zerocopy_hostpath.txt).
+std::atomic<uint64_t> g_last_caller[kMaxDevices];
+std::atomic<int64_t> g_other_caller_ns[kMaxDevices];
+constexpr int64_t kAloneNs = 20'000'000;
+
+bool lone_caller(int dev)
+{
+    static thread_local const uint64_t me = std::hash<std::thread::id>{}(std::this_thread::get_id()) | 1u;
+    const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                            std::chrono::steady_clock::now().time_since_epoch()).count();
+    if (g_last_caller[dev].exchange(me) != me) g_other_caller_ns[dev].store(now);
+    return now - g_other_caller_ns[dev].load() > kAloneNs;
+}
 // elect_ec_host_path_stats: zero-copy calls, zero-copy fallbacks, batched, per-thread engine.
 std::atomic<uint64_t> g_stats[4];
 
@@ -992,7 +1012,7 @@ int run_host(const HostOp& op, size_t len)
     } in_flight(g_in_flight[dev]);
     try {  // nothing may unwind into the JVM: allocation failures become status codes
         rc = Batcher::kFallback;
-        if (ZeroCopy::eligible(op, len, in_flight.now)) {
+        if (ZeroCopy::eligible(op, len, in_flight.now, lone_caller(dev))) {
             rc = ZeroCopy::run(op, len);
             g_stats[rc == ZeroCopy::kFallback ? 1 : 0].fetch_add(1);
             if (rc == ZeroCopy::kFallback) rc = Batcher::kFallback;

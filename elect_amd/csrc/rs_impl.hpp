@@ -955,9 +955,13 @@ __global__ __launch_bounds__(kBlock) void gf_apply_groupp(const GroupArgs<K, R> 
 }
 
 #ifndef AB_PAD_U4
-#define AB_PAD_U4 4
+#define AB_PAD_U4 2
 #endif
 // Segments per lane for gf_apply_lens: U*K 16-byte loads in flight per lane.
+// U = 2 since round 3 (3 interleaved rounds, profiles/r03/padded_and_plain_u_ab.txt):
+// ELECT's degraded read 77.3 -> 81.6 % of peak at 64 KiB codeLength and 80.7 ->
+// 82.2 % at 4.4 MB in 64 KiB tiles, padded encode at 93 % fill 79.1 -> 80.1 %,
+// full units 81.0 -> 82.3 %, random fill 69.1 -> 68.8 % (noise); U = 4 before.
 template <int K>
 constexpr int lens_unroll() { return K <= 4 ? AB_PAD_U4 : 1; }
 

@@ -210,7 +210,7 @@ for step in "$@"; do
     zerocopy) run zerocopy 600 python tools/tune/zerocopy_probe.py || exit $? ;;
     zchost)  # the product's host path with zero-copy lone callers: tests, then callers 1 / 2 / 16 / 64, on vs off
         run pytest_zerocopy 600 python -m pytest tests/test_gpu_zerocopy.py -x -q -p no:cacheprovider --timeout 300 || exit $?
-        for i in 1 2; do for z in 1 0; do for T in 1 2 16 64; do
+        for i in 1 2; do for z in 1 0; do for T in ${ZC_T:-1 2 16 64}; do
             ELECT_EC_ZEROCOPY=$z run "zchost_z${z}_T${T}_$i" 300 python bench.py --config hostpath --threads $T --host-seconds 2 || exit $?
         done; done; done ;;
     rs12gap)  # RS(12,8) decode inside the headline line vs its own --config run, interleaved
