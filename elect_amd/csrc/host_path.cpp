@@ -973,7 +973,8 @@ bool lone_caller(int dev)
     static thread_local const uint64_t me = std::hash<std::thread::id>{}(std::this_thread::get_id()) | 1u;
     const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
                             std::chrono::steady_clock::now().time_since_epoch()).count();
-    if (g_last_caller[dev].exchange(me) != me) g_other_caller_ns[dev].store(now);
+    const uint64_t prev = g_last_caller[dev].exchange(me);
+    if (prev != me && prev != 0) g_other_caller_ns[dev].store(now);  // 0: no thread has called before
     return now - g_other_caller_ns[dev].load() > kAloneNs;
 }
 // elect_ec_host_path_stats: zero-copy calls, zero-copy fallbacks, batched, per-thread engine.
