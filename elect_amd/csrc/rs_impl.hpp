@@ -1028,8 +1028,8 @@ constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches ar
 #define AB_WAVES_WRITE_HEAVY 24
 #endif
 constexpr size_t kLdsPerCU = 160 * 1024;
-#ifndef AB_PERSIST
-#define AB_PERSIST 0
+#ifndef AB_PERSIST  // A/B builds only (tools/ab_build.sh NAME -DAB_PERSIST=1): compile the persistent
+#define AB_PERSIST 0   // kernels, chosen at run time by ELECT_EC_PERSIST; measured slower
 #endif
 #ifndef AB_PLAIN_U  // A/B: segments per lane of plain (per-lane addressed) launches; 1 = gf_apply_x16
 #define AB_PLAIN_U 1
@@ -1067,13 +1067,14 @@ inline size_t cap_lds(int block, int coefs, int waves)
     return per_block > static_lds ? per_block - static_lds : 0;
 }
 
-// Persistent launches (gf_apply_x16p / gf_apply_groupp): ELECT_EC_PERSIST = 0
-// (off), 1 (plain and grouped launches) or 2 (grouped only); read once.
+// Persistent launches (gf_apply_x16p / gf_apply_groupp), in AB_PERSIST builds only:
+// ELECT_EC_PERSIST = 0 (off), 1 (plain and grouped launches) or 2 (grouped only); read once.
 inline int persist_mode()
 {
+    if constexpr (AB_PERSIST == 0) return 0;
     static const int m = [] {
         const char* e = std::getenv("ELECT_EC_PERSIST");
-        return e ? std::atoi(e) : AB_PERSIST;
+        return e ? std::atoi(e) : 0;
     }();
     return m;
 }
@@ -1235,8 +1236,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                                        dim3(block), cap_lds(block, R * K, AB_PLAIN_U_WAVES ? AB_PLAIN_U_WAVES : plain_waves_cap(K, R)),
                                        stream, a);
                 }
-            } else if (!PAD && !a.hashes && persist_mode() == 1) {  // persistent form (gf_apply_x16p)
-                if constexpr (!PAD) {
+            } else if (AB_PERSIST && !PAD && !a.hashes && persist_mode() == 1) {  // persistent form (gf_apply_x16p)
+                if constexpr (!PAD && AB_PERSIST != 0) {
                     const int waves = plain_waves_cap(K, R);
                     const dim3 pg(persist_grid(grid, block, waves));
                     const size_t lds = cap_lds(block, R * K, waves);
@@ -1338,19 +1339,21 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
         blocks += (g.total + block - 1) / block;
     }
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    if (persist_mode() >= 1) {  // persistent form (gf_apply_groupp)
-        const int waves = plain_waves_cap(K, R);
-        const dim3 pg(persist_grid(blocks, block, waves));
-        const size_t lds = cap_lds(block, R * K, waves);
-        const uint32_t vb = static_cast<uint32_t>(blocks);
-        if constexpr (K >= AB_SCALAR_BASE_MIN_K) {
-            if (uni) {
-                hipLaunchKernelGGL((gf_apply_groupp<K, R, true>), pg, dim3(block), lds, stream, a, vb);
-                return hipGetLastError();
+    if constexpr (AB_PERSIST != 0) {
+        if (persist_mode() >= 1) {  // persistent form (gf_apply_groupp)
+            const int waves = plain_waves_cap(K, R);
+            const dim3 pg(persist_grid(blocks, block, waves));
+            const size_t lds = cap_lds(block, R * K, waves);
+            const uint32_t vb = static_cast<uint32_t>(blocks);
+            if constexpr (K >= AB_SCALAR_BASE_MIN_K) {
+                if (uni) {
+                    hipLaunchKernelGGL((gf_apply_groupp<K, R, true>), pg, dim3(block), lds, stream, a, vb);
+                    return hipGetLastError();
+                }
             }
+            hipLaunchKernelGGL((gf_apply_groupp<K, R, false>), pg, dim3(block), lds, stream, a, vb);
+            return hipGetLastError();
         }
-        hipLaunchKernelGGL((gf_apply_groupp<K, R, false>), pg, dim3(block), lds, stream, a, vb);
-        return hipGetLastError();
     }
     if constexpr (K >= AB_SCALAR_BASE_MIN_K) {
         if (uni) {

@@ -199,14 +199,16 @@ for step in "$@"; do
                     -- python3 bench.py --config padded --pad-fill $fill --steps 20 || exit $?
             done
         done ;;
-    persist)  # persistent plain/grouped kernels (ELECT_EC_PERSIST): GPU suite under it, then interleaved A/B
+    persist)  # persistent plain/grouped kernels (build first: tools/ab_build.sh persist -DAB_PERSIST=1; ELECT_EC_LIB=elect_amd/_ab/libelect_ec_persist.so ELECT_EC_PERSIST=1): GPU suite under it, then interleaved A/B
+        export ELECT_EC_LIB=$PWD/elect_amd/_ab/libelect_ec_persist.so
         ELECT_EC_PERSIST=1 run pytest_gpu_persist 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 || exit $?
         for i in 1 2 3; do for P in 0 1; do
             ELECT_EC_PERSIST=$P run "persist${P}_headline_$i" 300 python bench.py --no-cpu --no-host --no-configs --steps 50 || exit $?
             ELECT_EC_PERSIST=$P run "persist${P}_mixed8_$i" 300 python bench.py --config mixed --mixed-share 8 --steps 50 || exit $?
             ELECT_EC_PERSIST=$P run "persist${P}_mixed_$i" 300 python bench.py --config mixed --steps 50 || exit $?
             ELECT_EC_PERSIST=$P run "persist${P}_rs12_$i" 300 python bench.py --config rs12 --steps 50 || exit $?
-        done; done ;;
+        done; done
+        unset ELECT_EC_LIB ;;
     zerocopy) run zerocopy 600 python tools/tune/zerocopy_probe.py || exit $? ;;
     zchost)  # the product's host path with zero-copy lone callers: tests, then callers 1 / 2 / 16 / 64, on vs off
         run pytest_zerocopy 600 python -m pytest tests/test_gpu_zerocopy.py -x -q -p no:cacheprovider --timeout 300 || exit $?
