@@ -793,6 +793,7 @@ def config_hostpath(args, world, rank, dev):
 
 
 HOSTPATH_CALLERS = 64  # ELECT's concurrent_ec (conf/elect.yaml:598)
+HOSTPATH_CHILD_TIMEOUT_S = 420
 
 
 def hostpath_child_cmd(ndev: int) -> list:
@@ -828,7 +829,11 @@ def hostpath_all_devices(args, world, rank, child=None):
     if rank == 0:
         ndev = world if child is not None else min(world, torch.cuda.device_count())
         cmd = child if child is not None else hostpath_child_cmd(ndev)
-        r = subprocess.run(cmd, capture_output=True, text=True, env=child_env(), timeout=900)
+        try:  # (well inside the gloo group's 10-minute timeout the other ranks wait under)
+            r = subprocess.run(cmd, capture_output=True, text=True, env=child_env(), timeout=HOSTPATH_CHILD_TIMEOUT_S)
+        except subprocess.TimeoutExpired as e:
+            r = subprocess.CompletedProcess(cmd, -9, (e.stdout or b"").decode(errors="replace") if isinstance(
+                e.stdout, bytes) else (e.stdout or ""), f"timed out after {HOSTPATH_CHILD_TIMEOUT_S} s")
         line = next((x for x in reversed(r.stdout.splitlines()) if x.startswith("{")), None)
         if r.returncode != 0 or line is None:
             res = {"verified": False, "devices": ndev, "error": f"rc={r.returncode}: {(r.stderr or r.stdout)[-400:]}"}

@@ -115,6 +115,17 @@ def test_hostpath_child_command_and_env():
     assert env.get("PATH") == os.environ.get("PATH")
 
 
+def test_hostpath_child_timeout_is_a_record_not_a_crash():
+    """A host-path child that outlives its limit becomes an unverified record on
+    rank 0 (the line still prints, and fails), not an exception that would leave
+    the other ranks waiting at the barrier; the limit sits inside the gloo timeout."""
+    mod = _bench_module()
+    assert mod.HOSTPATH_CHILD_TIMEOUT_S < 10 * 60
+    mod.HOSTPATH_CHILD_TIMEOUT_S = 1
+    res = mod.hostpath_all_devices(None, 1, 0, child=[sys.executable, "-c", "import time; time.sleep(30)"])
+    assert res["verified"] is False and "timed out" in res["error"], res
+
+
 def test_cpu_baseline_thread_points():
     """The CPU baseline sweeps the cgroup quota, twice it, 64 and the affinity
     mask (capped at the mask), and reports the best point, so a 16-CPU quota under
