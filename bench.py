@@ -270,6 +270,10 @@ def cpu_baseline(args, k, m, L, stripes):
         "kind": "port",
         "sweep": {str(p): round(v[2], 3) for p, v in sweep.items()},
         "single_core_GiB/s": round(reps1 * step_bytes / t1 / GIB, 3),
+        # core time per GiB coded on the CPU (best thread count, and one core): against the
+        # host path's cpu_core_ms_per_GiB, what offloading saves the node's cores
+        "core_ms_per_GiB": round(1e3 * best / rate, 2),
+        "single_core_ms_per_GiB": round(1e3 * t1 / (reps1 * step_bytes / GIB), 2),
         "working_set_bytes": int(buf.nbytes + out.nbytes),
         "cpu_model": info["model"],
         "affinity_cpus": info["affinity"],
@@ -737,16 +741,21 @@ def config_hostpath(args, world, rank, dev):
     fused = args.host_op == "encode_ex"
     content = [int(L / 1.05) - 64 * j for j in range(k)]  # SSTables just under codeLength/1.05
 
+    errors = []
+
     def worker(t, n):
-        if not args.host_devices:
-            torch.cuda.set_device(dev)
-        d, p = bufs[t]
-        da, pa = [x.ctypes.data for x in d], [x.ctypes.data for x in p]
-        for _ in range(n):
-            if fused:
-                coder.encode_ex_host(da, pa, L, data_lengths=content, hashed=True)
-            else:
-                coder.encode_host(da, pa, L)
+        try:
+            if not args.host_devices:
+                torch.cuda.set_device(dev)
+            d, p = bufs[t]
+            da, pa = [x.ctypes.data for x in d], [x.ctypes.data for x in p]
+            for _ in range(n):
+                if fused:
+                    coder.encode_ex_host(da, pa, L, data_lengths=content, hashed=True)
+                else:
+                    coder.encode_host(da, pa, L)
+        except Exception as e:  # a failed call fails the run (a thread's exception would vanish)
+            errors.append(f"caller {t}: {e!r}")
 
     def run(n):
         th = [threading.Thread(target=worker, args=(t, n)) for t in range(T)]
@@ -754,13 +763,19 @@ def config_hostpath(args, world, rank, dev):
             x.start()
         for x in th:
             x.join()
+        if errors:
+            raise RuntimeError(f"{len(errors)} caller(s) failed: {errors[0]}")
 
+    import resource
     run(1)  # warm: every caller's device, arenas and dispatchers
-    done, dt = 0, 0.0
+    done, dt, cpu = 0, 0.0, 0.0
     while done == 0 or dt < args.host_seconds:
+        r0 = resource.getrusage(resource.RUSAGE_SELF)
         t0 = time.perf_counter()
         run(calls)
         dt += time.perf_counter() - t0
+        r1 = resource.getrusage(resource.RUSAGE_SELF)
+        cpu += (r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)
         done += calls
     d, p = bufs[0]  # self-check through the product: rebuild d0 from [p0, d1, d2, d3]
     rebuilt = np.empty(L, np.uint8)
@@ -779,9 +794,14 @@ def config_hostpath(args, world, rank, dev):
     # caller's parity must at least equal caller 0's recomputation on its own data
     op_name = "fused encode step (zero fill + encode + parity hashCode, elect_ec_encode_ex)" if fused else \
         "encode"
+    data_gib = T * done * k * L / GIB
+    stats = _lib.host_path_stats()
     return {"metric": f"GiB/s host-memory RS(6,4) {op_name} through the C ABI (JNI calling convention)",
-            "value": round(T * done * k * L / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
-            "devices": ndev, "callers": T, "host_path_stats": _lib.host_path_stats(),
+            "value": round(data_gib / dt, 2), "unit": "GiB/s", "n_gpus": world,
+            "devices": ndev, "callers": T, "host_path_stats": stats,
+            # CPU time the whole process spent (every caller, helper and dispatcher thread) per GiB
+            # of data coded: what the offload costs the node's cores
+            "cpu_core_ms_per_GiB": round(cpu * 1e3 / data_gib, 2),
             "steps": done, "warmup": 1, "ms_per_step": round(dt / done * 1e3, 3), "higher_is_better": True,
             "scaling": "none", "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
             "config": {"workload": f"{T} threads x {done} synchronous elect_ec_{args.host_op} calls, one stripe "
@@ -842,6 +862,7 @@ def hostpath_all_devices(args, world, rank, child=None):
         else:
             o = json.loads(line)
             res = {"value": o["value"], "unit": o["unit"], "devices": o["devices"], "callers": o["callers"],
+                   "cpu_core_ms_per_GiB": o.get("cpu_core_ms_per_GiB"),
                    "host_path_stats": o.get("host_path_stats"),
                    "calls_per_caller": o["steps"], "verified": bool(o["verified"]),
                    "workload": o["config"]["workload"], "parallelism": o["config"]["parallelism"]}
