@@ -1027,6 +1027,21 @@ constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches ar
 #ifndef AB_WAVES_WRITE_HEAVY
 #define AB_WAVES_WRITE_HEAVY 24
 #endif
+// Read-heavy launches of 8 or more source columns (RS(12,8) decodes) keep twice
+// the read streams open per wave: 12 waves per CU there (round 3, interleaved
+// rounds on two boxes, profiles/r03/occupancy_wide_ab.txt): RS(12,8)
+// two-erasure decode at 20 / 16 / 14 / 12 / 10 / 8 waves 78.2 / 79.5 / 83.0 /
+// 85.2 / 75.7 / 75.7 % of peak (configs[4] 4,541 -> 4,935 GiB/s at 12, alone;
+// 4,458-4,489 -> 4,765-4,775 inside the headline line); 16 for every
+// read-heavy shape cost the mixed config's 1-4 KiB decodes 2-4 points.
+#ifndef AB_WAVES_READ_HEAVY_WIDE
+#define AB_WAVES_READ_HEAVY_WIDE 12
+#endif
+// (write-heavy ones of 8 or more columns keep 24: RS(12,8) encode at 16 / 12
+// waves 72.5 / 66.9 % against 74.6 %)
+#ifndef AB_WAVES_WRITE_HEAVY_WIDE  // A/B: write-heavy launches of 8 or more source columns (RS(12,8) encodes)
+#define AB_WAVES_WRITE_HEAVY_WIDE AB_WAVES_WRITE_HEAVY
+#endif
 constexpr size_t kLdsPerCU = 160 * 1024;
 #ifndef AB_PERSIST  // A/B builds only (tools/ab_build.sh NAME -DAB_PERSIST=1): compile the persistent
 #define AB_PERSIST 0   // kernels, chosen at run time by ELECT_EC_PERSIST; measured slower
@@ -1041,9 +1056,18 @@ constexpr size_t kLdsPerCU = 160 * 1024;
 #define AB_PLAIN_U_WAVES 0
 #endif
 
-inline int plain_waves_cap(int cols, int rows)
+// (and narrow read-heavy ones of 128-thread blocks, chunks <= 4 KiB, keep 20 too:
+// 1 KiB decodes at 16 / 24 waves 80.7 / 81.4 % against 82.4 %; write-heavy wide
+// ones at 28 / 32 waves measured the same as 24)
+#ifndef AB_WAVES_READ_HEAVY_SMALL  // A/B: narrow read-heavy launches of 128-thread blocks (chunks <= 4 KiB)
+#define AB_WAVES_READ_HEAVY_SMALL AB_WAVES_READ_HEAVY
+#endif
+
+inline int plain_waves_cap(int cols, int rows, int block)
 {
-    return 2 * rows >= cols ? AB_WAVES_WRITE_HEAVY : AB_WAVES_READ_HEAVY;
+    if (2 * rows >= cols) return cols >= 8 ? AB_WAVES_WRITE_HEAVY_WIDE : AB_WAVES_WRITE_HEAVY;
+    if (cols >= 8) return AB_WAVES_READ_HEAVY_WIDE;
+    return block < kBlock ? AB_WAVES_READ_HEAVY_SMALL : AB_WAVES_READ_HEAVY;
 }
 
 inline size_t cap_lds(int block, int coefs, int waves);
@@ -1055,7 +1079,9 @@ inline size_t cap_lds(int block, int coefs, int waves);
 #endif
 inline size_t lens_cap(int block, int coefs, int cols, int rows)
 {
-    return AB_CAP_LENS ? cap_lds(block, coefs, AB_CAP_LENS > 1 ? AB_CAP_LENS : plain_waves_cap(cols, rows)) : 0;
+    // (the wide caps above were measured on the plain kernels only)
+    const int waves = 2 * rows >= cols ? AB_WAVES_WRITE_HEAVY : AB_WAVES_READ_HEAVY;
+    return AB_CAP_LENS ? cap_lds(block, coefs, AB_CAP_LENS > 1 ? AB_CAP_LENS : waves) : 0;
 }
 
 inline size_t cap_lds(int block, int coefs, int waves)
@@ -1233,12 +1259,12 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                     constexpr int U = AB_PLAIN_U;
                     const uint64_t th = (static_cast<uint64_t>(a.total) + 64 * U - 1) / (64 * U) * 64;
                     hipLaunchKernelGGL((gf_apply_x16m<K, R, U>), dim3(static_cast<uint32_t>((th + block - 1) / block)),
-                                       dim3(block), cap_lds(block, R * K, AB_PLAIN_U_WAVES ? AB_PLAIN_U_WAVES : plain_waves_cap(K, R)),
+                                       dim3(block), cap_lds(block, R * K, AB_PLAIN_U_WAVES ? AB_PLAIN_U_WAVES : plain_waves_cap(K, R, block)),
                                        stream, a);
                 }
             } else if (AB_PERSIST && !PAD && !a.hashes && persist_mode() == 1) {  // persistent form (gf_apply_x16p)
                 if constexpr (!PAD && AB_PERSIST != 0) {
-                    const int waves = plain_waves_cap(K, R);
+                    const int waves = plain_waves_cap(K, R, block);
                     const dim3 pg(persist_grid(grid, block, waves));
                     const size_t lds = cap_lds(block, R * K, waves);
                     if constexpr (kPlainU) {
@@ -1254,7 +1280,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                 if constexpr (!PAD && kPlainU) {
                     if (!a.hashes)
                         hipLaunchKernelGGL((gf_apply_x16u<K, R, false>), dim3(grid), dim3(block),
-                                           cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
+                                           cap_lds(block, R * K, plain_waves_cap(K, R, block)), stream, a);
                 }
                 if constexpr (!PAD && K <= kMaxHashCols) {
                     if (a.hashes)
@@ -1262,7 +1288,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                 }
             } else if (!a.hashes) {
                 hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, false>), dim3(grid), dim3(block),
-                                   PAD ? 0 : cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
+                                   PAD ? 0 : cap_lds(block, R * K, plain_waves_cap(K, R, block)), stream, a);
             } else if constexpr (K <= kMaxHashCols) {
                 // (uncapped: capping the hashed instance at 24 / 28 waves per CU cost it 5 / 3
                 // points, and staging 31^(16*lane) in LDS instead of constant memory gained
@@ -1341,7 +1367,7 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
     if constexpr (AB_PERSIST != 0) {
         if (persist_mode() >= 1) {  // persistent form (gf_apply_groupp)
-            const int waves = plain_waves_cap(K, R);
+            const int waves = plain_waves_cap(K, R, block);
             const dim3 pg(persist_grid(blocks, block, waves));
             const size_t lds = cap_lds(block, R * K, waves);
             const uint32_t vb = static_cast<uint32_t>(blocks);
@@ -1358,12 +1384,12 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
     if constexpr (K >= AB_SCALAR_BASE_MIN_K) {
         if (uni) {
             hipLaunchKernelGGL((gf_apply_group<K, R, true>), dim3(static_cast<uint32_t>(blocks)), dim3(block),
-                               cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
+                               cap_lds(block, R * K, plain_waves_cap(K, R, block)), stream, a);
             return hipGetLastError();
         }
     }
     hipLaunchKernelGGL((gf_apply_group<K, R, false>), dim3(static_cast<uint32_t>(blocks)), dim3(block),
-                       cap_lds(block, R * K, plain_waves_cap(K, R)), stream, a);
+                       cap_lds(block, R * K, plain_waves_cap(K, R, block)), stream, a);
     return hipGetLastError();
 }
 
