@@ -79,6 +79,8 @@ def parse():
                          "~20 ms of load, DESIGN.md §5); 0 = off")
     ap.add_argument("--per-step", action="store_true",
                     help="headline: also print every timed step's encode and decode kernel times (diagnostics)")
+    ap.add_argument("--rs12-erasures", type=int, default=2, choices=(1, 2, 3, 4),
+                    help="rs12: erase units 0..N-1, decode from the next 8 (BASELINE configs[4]: 2)")
     ap.add_argument("--configs-order", default="mixed,rs12",
                     help="headline: the BASELINE configs run after the headline phases, in this order")
     ap.add_argument("--no-sizes", action="store_true",
@@ -656,24 +658,25 @@ def config_rs12(args, world, rank, dev):
     from elect_amd.batch import decode_batch, encode_batch
     from elect_amd.coder import RSCoder
     k, m, L, B = 8, 4, 262144, 512
+    e = args.rs12_erasures
     coder = RSCoder(k, m)
     st, Bc, Lc = alloc_stripes(args, B, L, k, m, dev)  # layout policy of layout_for (64 KiB tiles)
     encode_batch(coder, st[:, :k], st[:, k:])
-    out = torch.empty((Bc, 2, Lc), dtype=torch.uint8, device=dev)
-    surv = list(range(2, 10))
+    out = torch.empty((Bc, e, Lc), dtype=torch.uint8, device=dev)
+    surv = list(range(e, e + k))
     evs = []
 
     def step():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        decode_batch(coder, st, surv, [0, 1], out, inputs_by_unit=True)
+        decode_batch(coder, st, surv, list(range(e)), out, inputs_by_unit=True)
         e1.record()
         evs.append((e0, e1))
 
     dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms)
     ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
-    ok = torch.equal(out, st[:, :2])
-    alg = B * (k + 2) * L
+    ok = torch.equal(out, st[:, :e])
+    alg = B * (k + e) * L
     gbs = alg / (ms * 1e-3) / 1e9
     # the same code's encode (k=8, m=4), outside the timed region: HIP events per launch
     par = st[:, k:].clone()
@@ -688,8 +691,9 @@ def config_rs12(args, world, rank, dev):
     ok = ok and torch.equal(par, st[:, k:])
     enc_ms = sorted(a.elapsed_time(b) for a, b in enc_ev)[len(enc_ev) // 2]
     enc_gbs = B * (k + m) * L / (enc_ms * 1e-3) / 1e9
-    return {"metric": "GiB/s device-resident RS(12,8) two-erasure decode, 256 KiB chunks",
-            "kernels": {"decode_2erasure": {"ms": round(ms, 4), "GB/s": round(gbs, 1),
+    name = {1: "single", 2: "two", 3: "three", 4: "four"}[e]
+    return {"metric": f"GiB/s device-resident RS(12,8) {name}-erasure decode, 256 KiB chunks",
+            "kernels": {f"decode_{e}erasure": {"ms": round(ms, 4), "GB/s": round(gbs, 1),
                                             "frac": round(gbs / HBM_PEAK_GBS, 4)},
                         "encode": {"ms": round(enc_ms, 4), "GB/s": round(enc_gbs, 1),
                                    "frac": round(enc_gbs / HBM_PEAK_GBS, 4)}},
@@ -700,9 +704,9 @@ def config_rs12(args, world, rank, dev):
             "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "gf_apply_x16<8,2> (decode)", "algorithmic_bytes_per_launch": alg},
+                         "kernel": f"gf_apply_x16u<8,{e}> (decode)", "algorithmic_bytes_per_launch": alg},
             **({"per_step_ms": [round(a.elapsed_time(b), 4) for a, b in evs[-args.steps:]]} if args.per_step else {}),
-            "config": {"workload": f"RS(12,8) decode erase {{0,1}} from {surv}, {B} x {L} B stripes per GPU",
+            "config": {"workload": f"RS(12,8) decode erase {set(range(e))} from {surv}, {B} x {L} B stripes per GPU",
                        "layout": LAYOUT_NAMES[layout_for(args, L)],
                        "parallelism": f"stripe-partitioned x{world}"}}
 

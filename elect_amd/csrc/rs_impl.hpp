@@ -1032,8 +1032,10 @@ constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches ar
 // rounds on two boxes, profiles/r03/occupancy_wide_ab.txt): RS(12,8)
 // two-erasure decode at 20 / 16 / 14 / 12 / 10 / 8 waves 78.2 / 79.5 / 83.0 /
 // 85.2 / 75.7 / 75.7 % of peak (configs[4] 4,541 -> 4,935 GiB/s at 12, alone;
-// 4,458-4,489 -> 4,765-4,775 inside the headline line); 16 for every
-// read-heavy shape cost the mixed config's 1-4 KiB decodes 2-4 points.
+// 4,458-4,489 -> 4,765-4,775 inside the headline line), three erasures 79.1 ->
+// 82.2 %; one erasure (8 coefficients, 256-thread blocks) keeps 20 (77.7 % at
+// 12 against 78.1 %); 16 for every read-heavy shape cost the mixed config's
+// 1-4 KiB decodes 2-4 points.
 #ifndef AB_WAVES_READ_HEAVY_WIDE
 #define AB_WAVES_READ_HEAVY_WIDE 12
 #endif
@@ -1066,7 +1068,7 @@ constexpr size_t kLdsPerCU = 160 * 1024;
 inline int plain_waves_cap(int cols, int rows, int block)
 {
     if (2 * rows >= cols) return cols >= 8 ? AB_WAVES_WRITE_HEAVY_WIDE : AB_WAVES_WRITE_HEAVY;
-    if (cols >= 8) return AB_WAVES_READ_HEAVY_WIDE;
+    if (cols >= 8 && rows >= 2) return AB_WAVES_READ_HEAVY_WIDE;  // (>= 16 coefficients: 128-thread blocks)
     return block < kBlock ? AB_WAVES_READ_HEAVY_SMALL : AB_WAVES_READ_HEAVY;
 }
 

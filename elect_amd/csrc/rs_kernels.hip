@@ -232,6 +232,10 @@ hipError_t launch_bytes(const ApplyParams& p, hipStream_t stream)
 // ---------------------------------------------------------------------------
 // Parity update: par_out[r] = par_in[r] ^ c_r * (old ^ new), fused.
 // ---------------------------------------------------------------------------
+#ifndef AB_WAVES_UPDATE  // A/B: occupancy cap of the plain parity update (0: uncapped)
+#define AB_WAVES_UPDATE 0
+#endif
+
 template <int R>
 struct UpdArgs {
     const uint8_t* op;
@@ -297,7 +301,7 @@ hipError_t launch_update_r(const UpdateParams& p, int r0, hipStream_t stream)
         }
         a.total = static_cast<uint32_t>(ns * segs64);
         const uint32_t grid = (a.total + kBlock - 1) / kBlock;
-        hipLaunchKernelGGL((gf_update_x16<R>), dim3(grid), dim3(kBlock), 0, stream, a);
+        hipLaunchKernelGGL((gf_update_x16<R>), dim3(grid), dim3(kBlock), cap_lds(kBlock, 0, AB_WAVES_UPDATE), stream, a);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
