@@ -1003,10 +1003,25 @@ constexpr int lens_unroll() { return K <= 4 ? AB_PAD_U4 : 1; }
 // and so did launches with >= 16 coefficients (RS(12,8) encode +2-3.5 %, decode
 // +1 %); RS(6,4) encode/decode lose 1-2 % with them (interleaved A/B runs).
 // Keeping the tables in SGPRs instead of LDS (no barrier) lost 1 % on RS(6,4).
+#ifndef AB_BLOCK_WIDE_READ  // A/B: read-heavy launches of >= 16 coefficients (RS(12,8) decodes)
+#define AB_BLOCK_WIDE_READ 128
+#endif
+// Write-heavy ones (RS(12,8) encodes) run 256-thread blocks since the occupancy
+// caps (round 3, 3 interleaved rounds, profiles/r03/block_wide_ab.txt): 64 /
+// 128 / 256 threads 75.5 / 73.9 / 76.8 % of peak; read-heavy ones keep 128
+// (64: the same within noise; 256: 78 % against 85 %).
+#ifndef AB_BLOCK_WIDE_WRITE  // A/B: write-heavy launches of >= 16 coefficients (RS(12,8) encodes)
+#define AB_BLOCK_WIDE_WRITE 256
+#endif
 #ifdef AB_BLOCK  // A/B builds (tools/ab_build.sh): one block size for every launch
-inline int block_for(uint64_t, int) { return AB_BLOCK; }
+inline int block_for(uint64_t, int, int) { return AB_BLOCK; }
 #else
-inline int block_for(uint64_t len, int coefs) { return (len <= 4096 || coefs >= 16) ? 128 : kBlock; }
+inline int block_for(uint64_t len, int cols, int rows)
+{
+    if (len <= 4096) return 128;
+    if (cols * rows >= 16) return 2 * rows >= cols ? AB_BLOCK_WIDE_WRITE : AB_BLOCK_WIDE_READ;
+    return kBlock;
+}
 #endif
 
 constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches are encodes
@@ -1203,7 +1218,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     a.hpow = pow31(p.hash_base);
     for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(p.coef[(r0 + r) * p.cols + j]);
-    const int block = block_for(p.len, R * K);
+    const int block = block_for(p.len, K, R);
     const bool hash_assign = p.hashes && p.hash_seed;  // launch_apply chose assign mode
     // stripes per launch keeping idx < 2^31, whole logical stripes (tiles) per launch
     const uint64_t per_launch = kMaxIndex / segs64 / tiles * tiles;
@@ -1327,7 +1342,7 @@ constexpr std::array<FastFn, kFastRows> fast_row_fns()
 #ifndef AB_GROUP_BLOCK
 #define AB_GROUP_BLOCK 0
 #endif
-inline int group_class(const ApplyParams& p) { return AB_GROUP_BLOCK < 0 ? block_for(p.len, p.rows * p.cols) : 0; }
+inline int group_class(const ApplyParams& p) { return AB_GROUP_BLOCK < 0 ? block_for(p.len, p.cols, std::min(p.rows, kFastRows)) : 0; }
 
 // Launch parts [0, n) of a group (all plain, vector-capable, whole segments,
 // same coefficients) for output rows r0 .. r0+R-1.
@@ -1341,7 +1356,7 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
     int block = kBlock;
     bool uni = true;  // (used for K >= AB_SCALAR_BASE_MIN_K)
     for (int i = 0; i < n; ++i) {
-        block = std::min(block, block_for(ps[i].len, R * K));
+        block = std::min(block, block_for(ps[i].len, K, R));
         uni = uni && (ps[i].len / 16) % 64 == 0 && ps[i].len < (uint64_t{1} << 32);
     }
     if (AB_GROUP_BLOCK > 0) block = AB_GROUP_BLOCK;
