@@ -1013,6 +1013,9 @@ constexpr int lens_unroll() { return K <= 4 ? AB_PAD_U4 : 1; }
 #ifndef AB_BLOCK_WIDE_WRITE  // A/B: write-heavy launches of >= 16 coefficients (RS(12,8) encodes)
 #define AB_BLOCK_WIDE_WRITE 256
 #endif
+#ifndef AB_BLOCK_HASH_PAD  // A/B: block size of padded launches with the parity hash
+#define AB_BLOCK_HASH_PAD 64
+#endif
 #ifdef AB_BLOCK  // A/B builds (tools/ab_build.sh): one block size for every launch
 inline int block_for(uint64_t, int, int) { return AB_BLOCK; }
 #else
@@ -1218,7 +1221,11 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     a.hpow = pow31(p.hash_base);
     for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(p.coef[(r0 + r) * p.cols + j]);
-    const int block = block_for(p.len, K, R);
+    // Padded launches with the parity hash (ELECT's fused encode and update steps)
+    // run one-wave blocks: the fused encode step 80.0 -> 81.4 % of peak at ELECT's
+    // codeLength (64 KiB tiles) and 74.7 -> 76.3 % at 64 KiB codeLength, the
+    // update step unchanged (round 3, profiles/r03/block_hash_pad_ab.txt).
+    const int block = PAD && p.hashes ? AB_BLOCK_HASH_PAD : block_for(p.len, K, R);
     const bool hash_assign = p.hashes && p.hash_seed;  // launch_apply chose assign mode
     // stripes per launch keeping idx < 2^31, whole logical stripes (tiles) per launch
     const uint64_t per_launch = kMaxIndex / segs64 / tiles * tiles;
