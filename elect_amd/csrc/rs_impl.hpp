@@ -1013,6 +1013,9 @@ constexpr int lens_unroll() { return K <= 4 ? AB_PAD_U4 : 1; }
 #ifndef AB_BLOCK_WIDE_WRITE  // A/B: write-heavy launches of >= 16 coefficients (RS(12,8) encodes)
 #define AB_BLOCK_WIDE_WRITE 256
 #endif
+#ifndef AB_WAVES_HASH_PAD  // A/B: occupancy cap of padded launches with the parity hash (0: uncapped)
+#define AB_WAVES_HASH_PAD 0
+#endif
 #ifndef AB_BLOCK_HASH_PAD  // A/B: block size of padded launches with the parity hash
 #define AB_BLOCK_HASH_PAD 64
 #endif
@@ -1267,7 +1270,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                     constexpr int UH = AB_LENS_HASH_U;
                     const uint64_t th = (static_cast<uint64_t>(a.total) + 64 * UH - 1) / (64 * UH) * 64;
                     hipLaunchKernelGGL((gf_apply_lens<K, R, UH, true>), dim3(static_cast<uint32_t>((th + block - 1) / block)),
-                                       dim3(block), 0, stream, a);
+                                       dim3(block), cap_lds(block, R * K, AB_WAVES_HASH_PAD), stream, a);
                 }
             }
         }
@@ -1317,7 +1320,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                 // (uncapped: capping the hashed instance at 24 / 28 waves per CU cost it 5 / 3
                 // points, and staging 31^(16*lane) in LDS instead of constant memory gained
                 // nothing; profiles/r02_hash_ab/)
-                hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, true>), dim3(grid), dim3(block), 0, stream, a);
+                hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, true>), dim3(grid), dim3(block),
+                                   PAD ? cap_lds(block, R * K, AB_WAVES_HASH_PAD) : 0, stream, a);
             }  // (launch_apply rejects hashed launches wider than kMaxHashCols)
         }
         hipError_t e = hipGetLastError();
@@ -1349,6 +1353,10 @@ constexpr std::array<FastFn, kFastRows> fast_row_fns()
 #ifndef AB_GROUP_BLOCK
 #define AB_GROUP_BLOCK 0
 #endif
+#ifndef AB_GROUP_SMALL_BLOCK  // A/B: block size of grouped launches under kSmallGroupBytes of source (kBlock: off)
+#define AB_GROUP_SMALL_BLOCK 64
+#endif
+constexpr uint64_t kSmallGroupBytes = uint64_t{1} << 29;
 inline int group_class(const ApplyParams& p) { return AB_GROUP_BLOCK < 0 ? block_for(p.len, p.cols, std::min(p.rows, kFastRows)) : 0; }
 
 // Launch parts [0, n) of a group (all plain, vector-capable, whole segments,
@@ -1362,10 +1370,18 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(ps[0].coef[(r0 + r) * ps[0].cols + j]);
     int block = kBlock;
     bool uni = true;  // (used for K >= AB_SCALAR_BASE_MIN_K)
+    uint64_t bytes = 0;  // source bytes of the launch
     for (int i = 0; i < n; ++i) {
         block = std::min(block, block_for(ps[i].len, K, R));
         uni = uni && (ps[i].len / 16) % 64 == 0 && ps[i].len < (uint64_t{1} << 32);
+        bytes += ps[i].len * ps[i].stripes * K;
     }
+    // Short grouped launches (a strong-scaled mixed step at 8 GPUs: tens of
+    // microseconds each) run one-wave blocks, for a finer tail: the mixed
+    // config's 8-way share (384 MiB of sources per launch) 4,198 -> 4,276 GiB/s;
+    // the 4-way share (768 MiB) and full size lose with them, so only below
+    // kSmallGroupBytes of source bytes (profiles/r03/group_small_block_ab.txt).
+    if (bytes < kSmallGroupBytes) block = std::min(block, AB_GROUP_SMALL_BLOCK);
     if (AB_GROUP_BLOCK > 0) block = AB_GROUP_BLOCK;
     uint64_t blocks = 0;
     for (int i = 0; i < n; ++i) {
