@@ -1016,6 +1016,9 @@ constexpr int lens_unroll() { return K <= 4 ? AB_PAD_U4 : 1; }
 #ifndef AB_WAVES_HASH_PAD  // A/B: occupancy cap of padded launches with the parity hash (0: uncapped)
 #define AB_WAVES_HASH_PAD 0
 #endif
+#ifndef AB_BLOCK_PAD_WRITE  // A/B: block size of unhashed padded write-heavy launches
+#define AB_BLOCK_PAD_WRITE 128
+#endif
 #ifndef AB_BLOCK_HASH_PAD  // A/B: block size of padded launches with the parity hash
 #define AB_BLOCK_HASH_PAD 64
 #endif
@@ -1228,7 +1231,13 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     // run one-wave blocks: the fused encode step 80.0 -> 81.4 % of peak at ELECT's
     // codeLength (64 KiB tiles) and 74.7 -> 76.3 % at 64 KiB codeLength, the
     // update step unchanged (round 3, profiles/r03/block_hash_pad_ab.txt).
-    const int block = PAD && p.hashes ? AB_BLOCK_HASH_PAD : block_for(p.len, K, R);
+    // Unhashed padded encodes (per-unit content lengths) run 128-thread blocks:
+    // 64 KiB units at random fill 70.2 -> 73.8 % of peak, at ELECT's fill (93 %)
+    // 80.2 -> 80.7 %, full 82.1 -> 82.4 %; padded decodes keep 256 (64 / 128 threads:
+    // -3 / -4 points) (profiles/r03/block_pad_ab.txt).
+    const int block = PAD && p.hashes ? AB_BLOCK_HASH_PAD
+                      : PAD && 2 * R >= K ? std::min(AB_BLOCK_PAD_WRITE, block_for(p.len, K, R))
+                                          : block_for(p.len, K, R);
     const bool hash_assign = p.hashes && p.hash_seed;  // launch_apply chose assign mode
     // stripes per launch keeping idx < 2^31, whole logical stripes (tiles) per launch
     const uint64_t per_launch = kMaxIndex / segs64 / tiles * tiles;
