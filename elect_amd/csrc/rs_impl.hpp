@@ -1103,10 +1103,13 @@ inline size_t cap_lds(int block, int coefs, int waves);
 #ifndef AB_CAP_LENS
 #define AB_CAP_LENS 1
 #endif
+#ifndef AB_WAVES_PAD_WRITE  // A/B: occupancy cap of padded write-heavy launches (per-stripe lengths)
+#define AB_WAVES_PAD_WRITE AB_WAVES_WRITE_HEAVY
+#endif
 inline size_t lens_cap(int block, int coefs, int cols, int rows)
 {
     // (the wide caps above were measured on the plain kernels only)
-    const int waves = 2 * rows >= cols ? AB_WAVES_WRITE_HEAVY : AB_WAVES_READ_HEAVY;
+    const int waves = 2 * rows >= cols ? AB_WAVES_PAD_WRITE : AB_WAVES_READ_HEAVY;
     return AB_CAP_LENS ? cap_lds(block, coefs, AB_CAP_LENS > 1 ? AB_CAP_LENS : waves) : 0;
 }
 
