@@ -1065,6 +1065,36 @@ constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches ar
 #endif
 // (write-heavy ones of 8 or more columns keep 24: RS(12,8) encode at 16 / 12
 // waves 72.5 / 66.9 % against 74.6 %)
+// Plain launches (no padding, no hash) of chunks above 4 KiB and fewer than 16
+// coefficients run one-wave blocks, their cap set in single waves: RS(6,4)
+// encode at 16 waves per CU 82.4-82.6 -> 83.6-84.2 % of peak (14: 82.0, 12:
+// 75.7 %), RS(6,4) single-erasure decode at 17-18 waves 80.8-82.0 -> 83.8-84.1 %
+// (15: 80.7 %), RS(12,8) single-erasure decode at 12 waves 78.8-79.0 -> 84.8-85.0 %
+// (profiles/r03/plain_one_wave_ab.txt).  Finer block steps place the cap where
+// 256-thread blocks (4 waves a step) cannot.  Padded, hashed and grouped
+// launches keep their own shapes (padded decodes and full-size groups lose with
+// one-wave blocks).
+#ifndef AB_PLAIN_ONE_WAVE  // A/B: 0 = off
+#define AB_PLAIN_ONE_WAVE 1
+#endif
+#ifndef AB_WAVES_PLAIN_WRITE
+#define AB_WAVES_PLAIN_WRITE 18
+#endif
+#ifndef AB_WAVES_PLAIN_READ
+#define AB_WAVES_PLAIN_READ 18
+#endif
+#ifndef AB_WAVES_PLAIN_READ_WIDE
+#define AB_WAVES_PLAIN_READ_WIDE 12
+#endif
+inline bool plain_one_wave(uint64_t len, int cols, int rows)
+{
+    return AB_PLAIN_ONE_WAVE && len > 4096 && cols * rows < 16;
+}
+inline int plain_one_wave_cap(int cols, int rows)
+{
+    if (2 * rows >= cols) return AB_WAVES_PLAIN_WRITE;
+    return cols >= 8 ? AB_WAVES_PLAIN_READ_WIDE : AB_WAVES_PLAIN_READ;
+}
 #ifndef AB_WAVES_WRITE_HEAVY_WIDE  // A/B: write-heavy launches of 8 or more source columns (RS(12,8) encodes)
 #define AB_WAVES_WRITE_HEAVY_WIDE AB_WAVES_WRITE_HEAVY
 #endif
@@ -1238,9 +1268,12 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     // 64 KiB units at random fill 70.2 -> 73.8 % of peak, at ELECT's fill (93 %)
     // 80.2 -> 80.7 %, full 82.1 -> 82.4 %; padded decodes keep 256 (64 / 128 threads:
     // -3 / -4 points) (profiles/r03/block_pad_ab.txt).
-    const int block = PAD && p.hashes ? AB_BLOCK_HASH_PAD
+    const bool one_wave = !PAD && !p.hashes && plain_one_wave(p.len, K, R);
+    const int block = one_wave ? 64
+                      : PAD && p.hashes ? AB_BLOCK_HASH_PAD
                       : PAD && 2 * R >= K ? std::min(AB_BLOCK_PAD_WRITE, block_for(p.len, K, R))
                                           : block_for(p.len, K, R);
+    const int plain_cap = one_wave ? plain_one_wave_cap(K, R) : plain_waves_cap(K, R, block);
     const bool hash_assign = p.hashes && p.hash_seed;  // launch_apply chose assign mode
     // stripes per launch keeping idx < 2^31, whole logical stripes (tiles) per launch
     const uint64_t per_launch = kMaxIndex / segs64 / tiles * tiles;
@@ -1298,12 +1331,12 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                     constexpr int U = AB_PLAIN_U;
                     const uint64_t th = (static_cast<uint64_t>(a.total) + 64 * U - 1) / (64 * U) * 64;
                     hipLaunchKernelGGL((gf_apply_x16m<K, R, U>), dim3(static_cast<uint32_t>((th + block - 1) / block)),
-                                       dim3(block), cap_lds(block, R * K, AB_PLAIN_U_WAVES ? AB_PLAIN_U_WAVES : plain_waves_cap(K, R, block)),
+                                       dim3(block), cap_lds(block, R * K, AB_PLAIN_U_WAVES ? AB_PLAIN_U_WAVES : plain_cap),
                                        stream, a);
                 }
             } else if (AB_PERSIST && !PAD && !a.hashes && persist_mode() == 1) {  // persistent form (gf_apply_x16p)
                 if constexpr (!PAD && AB_PERSIST != 0) {
-                    const int waves = plain_waves_cap(K, R, block);
+                    const int waves = plain_cap;
                     const dim3 pg(persist_grid(grid, block, waves));
                     const size_t lds = cap_lds(block, R * K, waves);
                     if constexpr (kPlainU) {
@@ -1319,7 +1352,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                 if constexpr (!PAD && kPlainU) {
                     if (!a.hashes)
                         hipLaunchKernelGGL((gf_apply_x16u<K, R, false>), dim3(grid), dim3(block),
-                                           cap_lds(block, R * K, plain_waves_cap(K, R, block)), stream, a);
+                                           cap_lds(block, R * K, plain_cap), stream, a);
                 }
                 if constexpr (!PAD && K <= kMaxHashCols) {
                     if (a.hashes)
@@ -1327,7 +1360,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                 }
             } else if (!a.hashes) {
                 hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, false>), dim3(grid), dim3(block),
-                                   PAD ? 0 : cap_lds(block, R * K, plain_waves_cap(K, R, block)), stream, a);
+                                   PAD ? 0 : cap_lds(block, R * K, plain_cap), stream, a);
             } else if constexpr (K <= kMaxHashCols) {
                 // (uncapped: capping the hashed instance at 24 / 28 waves per CU cost it 5 / 3
                 // points, and staging 31^(16*lane) in LDS instead of constant memory gained
