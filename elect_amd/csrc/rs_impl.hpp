@@ -1086,9 +1086,19 @@ constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches ar
 #ifndef AB_WAVES_PLAIN_READ_WIDE
 #define AB_WAVES_PLAIN_READ_WIDE 12
 #endif
+#ifndef AB_PLAIN_ONE_WAVE_SMALL  // A/B: chunks <= 4 KiB too (1 = on)
+#define AB_PLAIN_ONE_WAVE_SMALL 0
+#endif
+// Grouped launches of one-wave blocks (short groups, kSmallGroupBytes) take the
+// one-wave caps too: the mixed config's 8-way share 4,272 -> 4,397 GiB/s
+// (profiles/r03/plain_one_wave_ab.txt).  Chunks <= 4 KiB keep 128-thread blocks
+// (one-wave blocks there: 1 KiB encode -0.6, decode +1 point, the same value).
+#ifndef AB_GROUP_ONE_WAVE_CAPS  // A/B: 0 = the caps of plain_waves_cap
+#define AB_GROUP_ONE_WAVE_CAPS 1
+#endif
 inline bool plain_one_wave(uint64_t len, int cols, int rows)
 {
-    return AB_PLAIN_ONE_WAVE && len > 4096 && cols * rows < 16;
+    return AB_PLAIN_ONE_WAVE && (len > 4096 || AB_PLAIN_ONE_WAVE_SMALL) && cols * rows < 16;
 }
 inline int plain_one_wave_cap(int cols, int rows)
 {
@@ -1428,6 +1438,8 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
     // kSmallGroupBytes of source bytes (profiles/r03/group_small_block_ab.txt).
     if (bytes < kSmallGroupBytes) block = std::min(block, AB_GROUP_SMALL_BLOCK);
     if (AB_GROUP_BLOCK > 0) block = AB_GROUP_BLOCK;
+    const int group_cap = AB_GROUP_ONE_WAVE_CAPS && block == 64 && K * R < 16 ? plain_one_wave_cap(K, R)
+                                                                              : plain_waves_cap(K, R, block);
     uint64_t blocks = 0;
     for (int i = 0; i < n; ++i) {
         const ApplyParams& p = ps[i];
@@ -1452,7 +1464,7 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
     if constexpr (AB_PERSIST != 0) {
         if (persist_mode() >= 1) {  // persistent form (gf_apply_groupp)
-            const int waves = plain_waves_cap(K, R, block);
+            const int waves = group_cap;
             const dim3 pg(persist_grid(blocks, block, waves));
             const size_t lds = cap_lds(block, R * K, waves);
             const uint32_t vb = static_cast<uint32_t>(blocks);
@@ -1469,12 +1481,12 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
     if constexpr (K >= AB_SCALAR_BASE_MIN_K) {
         if (uni) {
             hipLaunchKernelGGL((gf_apply_group<K, R, true>), dim3(static_cast<uint32_t>(blocks)), dim3(block),
-                               cap_lds(block, R * K, plain_waves_cap(K, R, block)), stream, a);
+                               cap_lds(block, R * K, group_cap), stream, a);
             return hipGetLastError();
         }
     }
     hipLaunchKernelGGL((gf_apply_group<K, R, false>), dim3(static_cast<uint32_t>(blocks)), dim3(block),
-                       cap_lds(block, R * K, plain_waves_cap(K, R, block)), stream, a);
+                       cap_lds(block, R * K, group_cap), stream, a);
     return hipGetLastError();
 }
 
