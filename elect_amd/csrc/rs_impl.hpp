@@ -1086,6 +1086,9 @@ constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches ar
 #ifndef AB_WAVES_PLAIN_READ_WIDE
 #define AB_WAVES_PLAIN_READ_WIDE 12
 #endif
+#ifndef AB_PAD_READ_ONE_WAVE  // A/B: padded read-heavy launches in one-wave blocks at this cap (0 = off)
+#define AB_PAD_READ_ONE_WAVE 0
+#endif
 #ifndef AB_PLAIN_ONE_WAVE_SMALL  // A/B: chunks <= 4 KiB too (1 = on)
 #define AB_PLAIN_ONE_WAVE_SMALL 0
 #endif
@@ -1149,7 +1152,7 @@ inline size_t cap_lds(int block, int coefs, int waves);
 inline size_t lens_cap(int block, int coefs, int cols, int rows)
 {
     // (the wide caps above were measured on the plain kernels only)
-    const int waves = 2 * rows >= cols ? AB_WAVES_PAD_WRITE : AB_WAVES_READ_HEAVY;
+    const int waves = 2 * rows >= cols ? AB_WAVES_PAD_WRITE : (AB_PAD_READ_ONE_WAVE ? AB_PAD_READ_ONE_WAVE : AB_WAVES_READ_HEAVY);
     return AB_CAP_LENS ? cap_lds(block, coefs, AB_CAP_LENS > 1 ? AB_CAP_LENS : waves) : 0;
 }
 
@@ -1279,7 +1282,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     // 80.2 -> 80.7 %, full 82.1 -> 82.4 %; padded decodes keep 256 (64 / 128 threads:
     // -3 / -4 points) (profiles/r03/block_pad_ab.txt).
     const bool one_wave = !PAD && !p.hashes && plain_one_wave(p.len, K, R);
-    const int block = one_wave ? 64
+    const bool pad_read_one_wave = AB_PAD_READ_ONE_WAVE && PAD && !p.hashes && 2 * R < K;
+    const int block = one_wave || pad_read_one_wave ? 64
                       : PAD && p.hashes ? AB_BLOCK_HASH_PAD
                       : PAD && 2 * R >= K ? std::min(AB_BLOCK_PAD_WRITE, block_for(p.len, K, R))
                                           : block_for(p.len, K, R);
@@ -1411,7 +1415,10 @@ constexpr std::array<FastFn, kFastRows> fast_row_fns()
 #ifndef AB_GROUP_SMALL_BLOCK  // A/B: block size of grouped launches under kSmallGroupBytes of source (kBlock: off)
 #define AB_GROUP_SMALL_BLOCK 64
 #endif
-constexpr uint64_t kSmallGroupBytes = uint64_t{1} << 29;
+#ifndef AB_SMALL_GROUP_BYTES  // A/B: groups of at least this many source bytes keep the larger blocks
+#define AB_SMALL_GROUP_BYTES (~uint64_t{0})
+#endif
+constexpr uint64_t kSmallGroupBytes = AB_SMALL_GROUP_BYTES;
 inline int group_class(const ApplyParams& p) { return AB_GROUP_BLOCK < 0 ? block_for(p.len, p.cols, std::min(p.rows, kFastRows)) : 0; }
 
 // Launch parts [0, n) of a group (all plain, vector-capable, whole segments,
@@ -1431,11 +1438,13 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
         uni = uni && (ps[i].len / 16) % 64 == 0 && ps[i].len < (uint64_t{1} << 32);
         bytes += ps[i].len * ps[i].stripes * K;
     }
-    // Short grouped launches (a strong-scaled mixed step at 8 GPUs: tens of
-    // microseconds each) run one-wave blocks, for a finer tail: the mixed
-    // config's 8-way share (384 MiB of sources per launch) 4,198 -> 4,276 GiB/s;
-    // the 4-way share (768 MiB) and full size lose with them, so only below
-    // kSmallGroupBytes of source bytes (profiles/r03/group_small_block_ab.txt).
+    // Grouped launches run one-wave blocks with the one-wave caps of the plain
+    // launches.  With round 2's caps one-wave blocks won only for short groups
+    // (the mixed config's 8-way share: 4,198 -> 4,276 GiB/s; the 4-way share and
+    // full size lost, profiles/r03/group_small_block_ab.txt); with the one-wave
+    // caps they win at every size: 8-way share 4,272 -> 4,397, 4-way 4,312 ->
+    // 4,461, 2-way 4,488 -> 4,568, full size 4,461 -> 4,531 GiB/s
+    // (profiles/r03/plain_one_wave_ab.txt).
     if (bytes < kSmallGroupBytes) block = std::min(block, AB_GROUP_SMALL_BLOCK);
     if (AB_GROUP_BLOCK > 0) block = AB_GROUP_BLOCK;
     const int group_cap = AB_GROUP_ONE_WAVE_CAPS && block == 64 && K * R < 16 ? plain_one_wave_cap(K, R)
