@@ -232,8 +232,15 @@ hipError_t launch_bytes(const ApplyParams& p, hipStream_t stream)
 // ---------------------------------------------------------------------------
 // Parity update: par_out[r] = par_in[r] ^ c_r * (old ^ new), fused.
 // ---------------------------------------------------------------------------
+// The plain parity update runs one-wave blocks, 18 waves per CU, like the plain
+// encodes: 81.6 -> 84.2 % of peak (uncapped 256-thread blocks before; caps on
+// those, 20-28 waves, measured within noise; one-wave blocks at 16 / 22 waves:
+// 83.5 / 83.8 %; profiles/r03/plain_one_wave_ab.txt).
 #ifndef AB_WAVES_UPDATE  // A/B: occupancy cap of the plain parity update (0: uncapped)
-#define AB_WAVES_UPDATE 0
+#define AB_WAVES_UPDATE 18
+#endif
+#ifndef AB_BLOCK_UPDATE  // A/B: its block size
+#define AB_BLOCK_UPDATE 64
 #endif
 
 template <int R>
@@ -253,7 +260,7 @@ struct UpdArgs {
 template <int R>
 __global__ __launch_bounds__(kBlock) void gf_update_x16(const UpdArgs<R> a)
 {
-    const uint32_t idx = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= a.total) return;
     const uint32_t s = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
     const uint64_t b0 = static_cast<uint64_t>(idx - s * a.segs) * 16;
@@ -300,8 +307,9 @@ hipError_t launch_update_r(const UpdateParams& p, int r0, hipStream_t stream)
             a.pos[r] = p.par_out[r0 + r].stride;
         }
         a.total = static_cast<uint32_t>(ns * segs64);
-        const uint32_t grid = (a.total + kBlock - 1) / kBlock;
-        hipLaunchKernelGGL((gf_update_x16<R>), dim3(grid), dim3(kBlock), cap_lds(kBlock, 0, AB_WAVES_UPDATE), stream, a);
+        const uint32_t grid = (a.total + AB_BLOCK_UPDATE - 1) / AB_BLOCK_UPDATE;
+        hipLaunchKernelGGL((gf_update_x16<R>), dim3(grid), dim3(AB_BLOCK_UPDATE),
+                           cap_lds(AB_BLOCK_UPDATE, 0, AB_WAVES_UPDATE), stream, a);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
