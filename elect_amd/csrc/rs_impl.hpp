@@ -1086,6 +1086,17 @@ constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches ar
 #ifndef AB_WAVES_PLAIN_READ_WIDE
 #define AB_WAVES_PLAIN_READ_WIDE 12
 #endif
+// Unpadded hashed launches (the fused-hash encode) run one-wave blocks at 20
+// waves per CU: 80.7 -> 81.2 % of peak (one-wave uncapped 80.4, at 24 waves
+// 81.0 %; profiles/r03/plain_one_wave_ab.txt).  Unhashed padded encodes keep
+// 128-thread blocks: one-wave ones at 16-20 waves gain at ELECT's fill (93 %:
+// 80.4 -> 82.1 %) but lose at random fill (71.9 -> 69.5 %).
+#ifndef AB_BLOCK_HASH_PLAIN  // A/B: block size of unpadded hashed launches (0: block_for)
+#define AB_BLOCK_HASH_PLAIN 64
+#endif
+#ifndef AB_WAVES_HASH_PLAIN  // A/B: their occupancy cap (0: uncapped)
+#define AB_WAVES_HASH_PLAIN 20
+#endif
 #ifndef AB_PAD_READ_ONE_WAVE  // A/B: padded read-heavy launches in one-wave blocks at this cap (0 = off)
 #define AB_PAD_READ_ONE_WAVE 0
 #endif
@@ -1286,6 +1297,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     const int block = one_wave || pad_read_one_wave ? 64
                       : PAD && p.hashes ? AB_BLOCK_HASH_PAD
                       : PAD && 2 * R >= K ? std::min(AB_BLOCK_PAD_WRITE, block_for(p.len, K, R))
+                      : !PAD && p.hashes && AB_BLOCK_HASH_PLAIN ? AB_BLOCK_HASH_PLAIN
                                           : block_for(p.len, K, R);
     const int plain_cap = one_wave ? plain_one_wave_cap(K, R) : plain_waves_cap(K, R, block);
     const bool hash_assign = p.hashes && p.hash_seed;  // launch_apply chose assign mode
@@ -1370,7 +1382,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                 }
                 if constexpr (!PAD && K <= kMaxHashCols) {
                     if (a.hashes)
-                        hipLaunchKernelGGL((gf_apply_x16u<K, R, true>), dim3(grid), dim3(block), 0, stream, a);
+                        hipLaunchKernelGGL((gf_apply_x16u<K, R, true>), dim3(grid), dim3(block),
+                                           cap_lds(block, R * K, AB_WAVES_HASH_PLAIN), stream, a);
                 }
             } else if (!a.hashes) {
                 hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, false>), dim3(grid), dim3(block),
