@@ -999,10 +999,13 @@ constexpr int lens_unroll() { return K <= 4 ? AB_PAD_U4 : 1; }
     }
 }
 
-// Small chunks (<= 4 KiB per shard) ran 3-4 % faster with 128-thread blocks,
-// and so did launches with >= 16 coefficients (RS(12,8) encode +2-3.5 %, decode
-// +1 %); RS(6,4) encode/decode lose 1-2 % with them (interleaved A/B runs).
-// Keeping the tables in SGPRs instead of LDS (no barrier) lost 1 % on RS(6,4).
+// Block size by shape (the occupancy caps below are set per block size; the
+// per-family choices since round 3 are in DESIGN.md §4, launch shape table):
+// small chunks (<= 4 KiB per shard) run 128-thread blocks (3-4 % over 256 in
+// round 1; one-wave blocks measured the same in round 3), launches of >= 16
+// coefficients 128 (read-heavy) or 256 (write-heavy), and plain launches of
+// fewer coefficients one-wave blocks (plain_one_wave, below).  Keeping the
+// tables in SGPRs instead of LDS (no barrier) lost 1 % on RS(6,4).
 #ifndef AB_BLOCK_WIDE_READ  // A/B: read-heavy launches of >= 16 coefficients (RS(12,8) decodes)
 #define AB_BLOCK_WIDE_READ 128
 #endif
