@@ -1043,7 +1043,7 @@ def config_flows(args, world, rank, dev):
         def gather(src_view):  # tiles -> [B, c, L]
             c = src_view.shape[1]
             return src_view.reshape(B, T, c, tile).permute(0, 2, 1, 3).reshape(B, c, T * tile)[:, :, :L]
-        layout = f"[B][{T}][k+m][{tile}] (64 KiB tiles, {T * tile - L} B pad per unit)"
+        layout = f"[B][{T}][k+m][{tile}] ({tile // 1024} KiB tiles, {T * tile - L} B pad per unit)"
     else:
         pitch = (L + 255) & ~255  # 256-byte unit pitch: ELECT's 4,404,020 B (= 4 mod 16) would misalign units
         stripe = torch.empty((B, n, pitch), dtype=torch.uint8, device=dev)[:, :, :L]
