@@ -1222,8 +1222,12 @@ inline uint32_t persist_grid(uint64_t vblocks, int block, int waves)
 // 73.1 -> 74.2 %, update 74.6 -> 76.0 %; but ELECT's 4.4 MB codeLength in tiles lost
 // 2 points (79.5 -> 77.6 %), full hashed units 1 % (3,762 -> 3,725 GiB/s), and
 // 4 segments per lane (121 VGPRs) or 1 lost everywhere: those stay on gf_apply_x16.
+// Round 3: with one-wave blocks for padded hashed launches (AB_BLOCK_HASH_PAD) the
+// one-segment gf_apply_x16<.., PAD, HASH> beats it at 64 KiB codeLength too:
+// encode 76.0 -> 78.1 %, update 76.7 -> 78.5 % (U = 1 / 4 in one-wave blocks:
+// 72.6 / 73.5 % encode; profiles/r03/lens_hash_ab.txt), so the path is off.
 #ifndef AB_LENS_HASH
-#define AB_LENS_HASH 1
+#define AB_LENS_HASH 0
 #endif
 #ifndef AB_LENS_HASH_U
 #define AB_LENS_HASH_U 2
