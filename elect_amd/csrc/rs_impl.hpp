@@ -1232,6 +1232,9 @@ inline uint32_t persist_grid(uint64_t vblocks, int block, int waves)
 #ifndef AB_LENS_HASH_U
 #define AB_LENS_HASH_U 2
 #endif
+#ifndef AB_LENS_HASH_MIN_LEN  // A/B knob: the lens path only at or above this unit length
+#define AB_LENS_HASH_MIN_LEN 0
+#endif
 inline bool lens_eligible(const ApplyParams& p)
 {
     return p.aligned16 && p.len % 16 == 0 && p.len > 0 && p.len < (uint64_t{1} << 31);
@@ -1239,7 +1242,8 @@ inline bool lens_eligible(const ApplyParams& p)
 
 inline bool lens_hash_path(const ApplyParams& p)
 {
-    return AB_LENS_HASH && p.hashes && p.padded && p.lens && p.tiles <= 1 && p.cols <= 4 && lens_eligible(p);
+    return AB_LENS_HASH && p.hashes && p.padded && p.lens && p.tiles <= 1 && p.cols <= 4 &&
+           p.len >= AB_LENS_HASH_MIN_LEN && lens_eligible(p);
 }
 
 // gf_apply_x16u (and the grouped kernel's UNI form) for plain launches of
