@@ -222,31 +222,90 @@ def cpu_thread_points(info: dict) -> list:
     return sorted(p for p in pts if p >= 1)
 
 
+def parse_cpulist(text: str) -> list:
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11] (sysfs cpulist format)."""
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        out += list(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
+def numa_cpus() -> dict:
+    """{node: [cpu, ...]}: the CPUs of this process's affinity mask on each NUMA
+    node, one logical CPU per physical core first (SMT siblings after), so that a
+    placement of t threads on a node takes t distinct cores while it can."""
+    aff = os.sched_getaffinity(0)
+    nodes = {}
+    for path in sorted(glob.glob("/sys/devices/system/node/node[0-9]*")):
+        try:
+            with open(os.path.join(path, "cpulist")) as f:
+                cpus = [c for c in parse_cpulist(f.read()) if c in aff]
+        except (OSError, ValueError):
+            continue
+        first, later = [], []
+        for c in cpus:
+            try:
+                with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                    primary = min(parse_cpulist(f.read())) == c
+            except (OSError, ValueError):
+                primary = True
+            (first if primary else later).append(c)
+        if cpus:
+            nodes[int(path.rsplit("node", 1)[1])] = first + later
+    return nodes
+
+
+def cpu_placements(info: dict) -> list:
+    """(name, threads, cpu set or None) points of the CPU baseline sweep: the thread
+    counts of cpu_thread_points() unpinned (the scheduler's choice inside the
+    affinity mask), and the quota and twice it pinned to one NUMA node's cores (each
+    node) and split evenly over two nodes.  A cgroup CPU quota (cpu.max) caps the
+    CPU time, not the CPUs: unpinned threads may wander over both sockets, away from
+    their pages."""
+    pts = [("any", t, None) for t in cpu_thread_points(info)]
+    nodes = numa_cpus()
+    q = math.ceil(info["quota_cores"]) if info.get("quota_cores") else min(16, info["affinity"])
+    for t in sorted({q, 2 * q}):
+        for n, cpus in sorted(nodes.items()):
+            if len(cpus) >= t:
+                pts.append((f"node{n}", t, cpus[:t]))
+        if len(nodes) >= 2:
+            (n0, c0), (n1, c1) = sorted(nodes.items())[:2]
+            if len(c0) >= t // 2 and len(c1) >= t - t // 2:
+                pts.append((f"split{n0}+{n1}", t, c0[:t // 2] + c1[:t - t // 2]))
+    return pts
+
+
 def cpu_baseline(args, k, m, L, stripes):
     """Oracle SIMD path (ISA-L's algorithm restated) on the host cores: the same
     encode + single-erasure decode step over the same stripe batch the GPU codes
     (4096 x 64 KiB: 1 GiB of data, 1.75 GiB touched, far beyond any LLC), stripes
-    split evenly over the threads.  The thread count is swept (cpu_thread_points)
-    and the best point is the value; then the same loop on one thread.  Bounded
-    to about --cpu-seconds of threaded work in all."""
+    split evenly over the threads.  Thread count and placement are swept
+    (cpu_placements: unpinned, pinned to one NUMA node with its pages first
+    touched there, split over two nodes) and the best point is the value; then
+    the same loop on one thread.  Bounded to about --cpu-seconds of threaded work
+    in all."""
     import numpy as np
     from oracle import ec_oracle as orc
     info = host_cpu_info()
-    points = cpu_thread_points(info)
+    points = cpu_placements(info)
     n = k + m
-    buf = np.empty((stripes, n, L), np.uint8)
-    orc.fill_splitmix(0xE1EC7, buf)
+    base = np.empty((stripes, n, L), np.uint8)
+    orc.fill_splitmix(0xE1EC7, base)
     em = orc.cauchy_matrix(k, m)
     enc_coef = em[k:]
     rc, dec_coef = orc.decode_matrix(k, m, list(range(1, k + 1)), [0])
-    out = np.empty((stripes, 1, L), np.uint8)
     level = orc.simd_best()
     sstride = n * L
     enc_src = [j * L for j in range(k)]
     enc_dst = [(k + r) * L for r in range(m)]
     dec_src = [j * L for j in range(1, k + 1)]
+    home = os.sched_getaffinity(0)
 
-    def loop(nthreads, budget, min_reps):
+    def loop(buf, out, nthreads, budget, min_reps):
         t, reps = 0.0, 0
         while t < budget or reps < min_reps:
             t += orc.batch_apply(enc_coef, buf, sstride, enc_src, buf, sstride, enc_dst, L, stripes, nthreads, level)
@@ -255,35 +314,58 @@ def cpu_baseline(args, k, m, L, stripes):
         return reps, t
 
     step_bytes = 2 * stripes * k * L
-    orc.batch_apply(enc_coef, buf, sstride, enc_src, buf, sstride, enc_dst, L, stripes, points[-1], level)  # warm
-    sweep = {}
-    for p in points:
-        reps, t = loop(p, args.cpu_seconds / len(points), 2)
-        sweep[p] = (reps, t, reps * step_bytes / t / GIB)
-    best = max(sweep, key=lambda p: sweep[p][2])
-    assert np.array_equal(out[:, 0], buf[:, 0]), "CPU baseline decode mismatch"
-    reps1, t1 = loop(1, args.cpu_seconds * 0.3, 1)  # single-core figure
-    reps, total_t, rate = sweep[best]
+    sweep, ok = {}, True
+    node_bufs = {}  # per pinned CPU set: the batch's pages first touched by a thread on those CPUs
+    budget = args.cpu_seconds / len(points)
+    try:
+        for name, t, cpus in points:
+            if cpus is None:
+                os.sched_setaffinity(0, home)
+                buf = base
+            else:
+                os.sched_setaffinity(0, cpus)  # this thread; the oracle's threads inherit it
+                key = tuple(sorted(cpus))
+                if key not in node_bufs:
+                    node_bufs.clear()  # one copy at a time (1.75 GiB each)
+                    b = np.empty_like(base)
+                    np.copyto(b, base)
+                    node_bufs[key] = b
+                buf = node_bufs[key]
+            out = np.empty((stripes, 1, L), np.uint8)
+            orc.batch_apply(enc_coef, buf, sstride, enc_src, buf, sstride, enc_dst, L, stripes, t, level)  # warm
+            reps, tt = loop(buf, out, t, budget, 2)
+            sweep[f"{name}:{t}"] = (reps, tt, reps * step_bytes / tt / GIB, name, t)
+            ok = ok and np.array_equal(out[:, 0], buf[:, 0])
+    finally:
+        os.sched_setaffinity(0, home)
+        node_bufs.clear()
+    assert ok, "CPU baseline decode mismatch"
+    best = max(sweep, key=lambda key: sweep[key][2])
+    reps, total_t, rate, place, threads = sweep[best]
+    out = np.empty((stripes, 1, L), np.uint8)
+    reps1, t1 = loop(base, out, 1, args.cpu_seconds * 0.3, 1)  # single-core figure
     return {
         "value": round(rate, 3),
         "unit": "GiB/s",
-        "cores": best,
-        "threads_used": best,
+        "cores": threads,
+        "threads_used": threads,
+        "placement": place,
         "kind": "port",
-        "sweep": {str(p): round(v[2], 3) for p, v in sweep.items()},
+        "sweep": {key: round(v[2], 3) for key, v in sweep.items()},
         "single_core_GiB/s": round(reps1 * step_bytes / t1 / GIB, 3),
-        # core time per GiB coded on the CPU (best thread count, and one core): against the
+        # core time per GiB coded on the CPU (best point, and one core): against the
         # host path's cpu_core_ms_per_GiB, what offloading saves the node's cores
-        "core_ms_per_GiB": round(1e3 * best / rate, 2),
+        "core_ms_per_GiB": round(1e3 * threads / rate, 2),
         "single_core_ms_per_GiB": round(1e3 * t1 / (reps1 * step_bytes / GIB), 2),
-        "working_set_bytes": int(buf.nbytes + out.nbytes),
+        "working_set_bytes": int(base.nbytes + out.nbytes),
         "cpu_model": info["model"],
         "affinity_cpus": info["affinity"],
         "cgroup_quota_cores": info["quota_cores"],
+        "numa_nodes": len(numa_cpus()),
         "sample": f"RS({n},{k}) encode + decode (erase 0) of the GPU's batch: {stripes} stripes x {L} B "
-                  f"({stripes * k * L / GIB:.2f} GiB data); threads swept over {points}, best {best}: {reps} reps "
-                  f"in {total_t:.1f} s; {reps1} reps in {t1:.1f} s on 1; oracle {orc.simd_name(level)} "
-                  f"(ISA-L's algorithm)",
+                  f"({stripes * k * L / GIB:.2f} GiB data); placement:threads swept over {list(sweep)}, best "
+                  f"{best}: {reps} reps in {total_t:.1f} s; {reps1} reps in {t1:.1f} s on 1; oracle "
+                  f"{orc.simd_name(level)} (ISA-L's algorithm)",
     }
 
 
@@ -431,6 +513,49 @@ def device_copy_rate(dev, nbytes=1 << 30, reps=5):
     ms = e0.elapsed_time(e1) / reps
     del a, b
     return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
+
+
+PROBE_SHAPES = ((256, 0), (64, 18))  # (block, waves per CU): tools/tune/tune_apply's probe; the plain coding launches
+
+
+def hbm_ceilings(dev, nbytes=1 << 31, reps=9):
+    """The HBM ceilings the coding kernels are judged against, measured on this GPU
+    by the library's own probe kernels (elect_ec_hbm_probe: 16 bytes per lane, the
+    coding kernels' non-temporal loads and stores) over 2 GiB buffers: read, write
+    and copy (read + write bytes counted), each the best of two launch shapes
+    (PROBE_SHAPES) by the median of `reps` launches timed with HIP events on the
+    stream they run on.  The achievable figures beside the 8 TB/s spec peak."""
+    from elect_amd import _lib
+    a = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    sink = torch.zeros(256, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    kinds = {"read": (0, a, sink, 1), "write": (1, None, b, 1), "copy": (2, a, b, 2)}
+    res = {}
+    for name, (kind, src, dst, mult) in kinds.items():
+        best = 0.0
+        for block, waves in PROBE_SHAPES:
+            def launch():
+                _lib.hbm_probe(kind, src.data_ptr() if src is not None else 0, dst.data_ptr(), nbytes, block, waves,
+                               stream.cuda_stream)
+            launch()
+            ts = []
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                launch()
+                e1.record(stream)
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            gbs = mult * nbytes / (sorted(ts)[reps // 2] * 1e-3) / 1e9
+            res[f"{name}_{block}x{waves}"] = round(gbs, 1)
+            best = max(best, gbs)
+        res[name] = round(best, 1)
+    if bool(sink.any()):
+        raise RuntimeError("hbm probe: the read probe's sink was written")
+    torch.cuda.synchronize()
+    del a, b, sink
+    return res
 
 
 def chunk_name(L: int) -> str:
@@ -800,12 +925,18 @@ def config_hostpath(args, world, rank, dev):
         "encode"
     data_gib = T * done * k * L / GIB
     stats = _lib.host_path_stats()
+    core_ms = cpu * 1e3 / data_gib
+    quota = host_cpu_info()["quota_cores"] or len(os.sched_getaffinity(0))
     return {"metric": f"GiB/s host-memory RS(6,4) {op_name} through the C ABI (JNI calling convention)",
             "value": round(data_gib / dt, 2), "unit": "GiB/s", "n_gpus": world,
             "devices": ndev, "callers": T, "host_path_stats": stats,
             # CPU time the whole process spent (every caller, helper and dispatcher thread) per GiB
             # of data coded: what the offload costs the node's cores
-            "cpu_core_ms_per_GiB": round(cpu * 1e3 / data_gib, 2),
+            "cpu_core_ms_per_GiB": round(core_ms, 2),
+            # the rate this path could reach if the process's CPU quota were its only limit
+            "cpu_bound_ceiling_GiB/s": round(quota * 1e3 / core_ms, 1) if core_ms > 0 else None,
+            "cpu_quota_cores": quota,
+            "host_wait": os.environ.get("ELECT_EC_HOST_WAIT", "block"),
             "steps": done, "warmup": 1, "ms_per_step": round(dt / done * 1e3, 3), "higher_is_better": True,
             "scaling": "none", "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
             "config": {"workload": f"{T} threads x {done} synchronous elect_ec_{args.host_op} calls, one stripe "
@@ -867,6 +998,8 @@ def hostpath_all_devices(args, world, rank, child=None):
             o = json.loads(line)
             res = {"value": o["value"], "unit": o["unit"], "devices": o["devices"], "callers": o["callers"],
                    "cpu_core_ms_per_GiB": o.get("cpu_core_ms_per_GiB"),
+                   "cpu_bound_ceiling_GiB/s": o.get("cpu_bound_ceiling_GiB/s"),
+                   "cpu_quota_cores": o.get("cpu_quota_cores"), "host_wait": o.get("host_wait"),
                    "host_path_stats": o.get("host_path_stats"),
                    "calls_per_caller": o["steps"], "verified": bool(o["verified"]),
                    "workload": o["config"]["workload"], "parallelism": o["config"]["parallelism"]}
@@ -1131,6 +1264,18 @@ def config_flows(args, world, rank, dev):
     valid = int(lens.sum().item())
     uvalid = int(ulens.sum().item())
     dvalid = int(dlens.sum().item())
+    # the layout's own ceiling for these kernels: a plain encode (no padding, no hash) of the
+    # same buffers (tiled: every tile whole), HIP events, median of 9 launches
+    pe = []
+    for _ in range(9):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        encode_batch(coder, data, par)
+        e1.record()
+        e1.synchronize()
+        pe.append(e0.elapsed_time(e1))
+    plain_ms = sorted(pe)[4]
+    plain_alg = data.shape[0] * n * data.shape[2]
     alg = {"encode": valid + B * m * L, "update": uvalid + 2 * B * m * L, "decode": dvalid + B * L}
     kern = {}
     for nm in ("encode", "update", "decode"):
@@ -1145,6 +1290,9 @@ def config_flows(args, world, rank, dev):
             "ms_per_step": round(dt / args.steps * 1e3, 4), "host_submit_ms_per_step": round(submit, 4),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok, "kernels": kern,
+            "plain_encode_same_layout": {"ms": round(plain_ms, 4),
+                                         "frac": round(plain_alg / (plain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                         "note": "full units, no padding or hash: the layout's ceiling for the steps"},
             "roofline": {"bound": "hbm", "achieved": kern["encode"]["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": kern["encode"]["frac"], "traffic": None,
                          "kernel": "gf_apply_x16<4,2,PAD,HASH> (encode step)",
@@ -1413,7 +1561,18 @@ def main():
     if rank == 0:
         out["kernels"]["decode_sweep"] = sw = decode_sweep(coder, stripe, stream)
         rec["verified"] = rec["verified"] and all(v["verified"] for v in sw.values())
-        out["roofline"]["device_copy_GB/s"] = device_copy_rate(dev)
+        ceil = hbm_ceilings(dev)
+        rf = out["roofline"]
+        # the achievable ceilings on this GPU (the library's 16 B/lane nt probes), and the
+        # coding kernels as fractions of them; torch's own copy kernel kept for reference
+        rf["device_copy_GB/s"] = ceil["copy"]
+        rf["device_read_GB/s"] = ceil["read"]
+        rf["device_write_GB/s"] = ceil["write"]
+        rf["frac_of_copy"] = round(enc_gbs / ceil["copy"], 4)
+        rf["decode_frac_of_copy"] = round(dec_gbs / ceil["copy"], 4)
+        rf["frac_of_read"] = round(enc_gbs / ceil["read"], 4)
+        rf["ceiling_probes"] = {key: v for key, v in ceil.items() if "_" in key}
+        rf["torch_copy_GB/s"] = device_copy_rate(dev)
     if not args.no_host:  # every rank, over its own PCIe link, at the same time
         own_rate, agg = host_inclusive(coder, k, m, L, min(B, 4096), dev, world)
         rates = gather(own_rate, world)

@@ -73,6 +73,7 @@ SIGNATURES = [
     ("elect_ec_strerror", ctypes.c_char_p, [ctypes.c_int]),
     ("elect_ec_device_count", ctypes.c_int, [_ip]),
     ("elect_ec_unaligned_vector_ok", ctypes.c_int, [_ip]),
+    ("elect_ec_hbm_probe", ctypes.c_int, [ctypes.c_int, _cp, _cp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, _cp]),
     ("elect_ec_set_host_devices", ctypes.c_int, [_ip, ctypes.c_int]),
     ("elect_ec_set_batching", ctypes.c_int, [ctypes.c_int, ctypes.c_uint, ctypes.c_size_t]),
     ("elect_ec_host_path_stats", ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
@@ -182,6 +183,12 @@ def unaligned_vector_ok() -> bool:
     ok = ctypes.c_int(0)
     check(lib.elect_ec_unaligned_vector_ok(ctypes.byref(ok)), "unaligned_vector_ok")
     return bool(ok.value)
+
+
+def hbm_probe(kind: int, src: int, dst: int, nbytes: int, block: int = 256, waves_per_cu: int = 0,
+              stream: int = 0) -> None:
+    """Enqueue one HBM ceiling probe (elect_ec_hbm_probe): kind 0 read, 1 write, 2 copy."""
+    check(lib.elect_ec_hbm_probe(kind, src or None, dst, nbytes, block, waves_per_cu, stream or None), "hbm_probe")
 
 
 def set_host_devices(devices) -> None:

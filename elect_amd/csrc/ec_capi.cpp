@@ -274,6 +274,14 @@ int elect_ec_unaligned_vector_ok(int* ok)
     return ELECT_EC_OK;
 }
 
+int elect_ec_hbm_probe(int kind, const void* src, void* dst, size_t bytes, int block, int waves_per_cu, void* stream)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ELECT_EC_ENODEV;
+    return elect::host::map_hip(
+        elect::kern::hbm_probe(kind, src, dst, bytes, block, waves_per_cu, static_cast<hipStream_t>(stream)));
+}
+
 int elect_ec_device_count(int* count)
 {
     if (!count) return ELECT_EC_EINVAL;

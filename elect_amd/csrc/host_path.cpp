@@ -9,6 +9,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -25,6 +26,46 @@ namespace {
 
 using kern::ApplyParams;
 
+// How host threads wait for the device (ELECT_EC_HOST_WAIT, read once).  HIP's
+// default waits poll: a thread in hipStreamSynchronize / hipEventSynchronize,
+// and the runtime thread behind a hipLaunchHostFunc callback, each keep a core
+// busy for as long as the device works.  On ELECT's storage
+// node those cores are the coding pool's.
+//   block (default): events created with hipEventBlockingSync; every wait is a
+//     blocking event wait (the thread sleeps until the interrupt); the batcher's
+//     completions come from a completion thread waiting on such events.
+//   spin: the same structure with polling events (A/B only).
+//   callback: round 3's waits: hipStreamSynchronize and host-function callbacks
+//     (A/B only).
+enum class WaitMode { kBlock, kSpin, kCallback };
+
+WaitMode wait_mode()
+{
+    static const WaitMode m = [] {
+        const char* e = std::getenv("ELECT_EC_HOST_WAIT");
+        if (e && std::strcmp(e, "spin") == 0) return WaitMode::kSpin;
+        if (e && std::strcmp(e, "callback") == 0) return WaitMode::kCallback;
+        return WaitMode::kBlock;
+    }();
+    return m;
+}
+
+hipError_t make_wait_event(hipEvent_t* ev)
+{
+    const unsigned flags = hipEventDisableTiming | (wait_mode() == WaitMode::kBlock ? hipEventBlockingSync : 0u);
+    return hipEventCreateWithFlags(ev, flags);
+}
+
+// Waits until everything enqueued on `s` so far is done: a blocking wait on
+// `ev` (recorded here), or hipStreamSynchronize in callback mode.
+hipError_t wait_stream(hipStream_t s, hipEvent_t ev)
+{
+    if (wait_mode() == WaitMode::kCallback || !ev) return hipStreamSynchronize(s);
+    hipError_t e = hipEventRecord(ev, s);
+    if (e == hipSuccess) e = hipEventSynchronize(ev);
+    return e;
+}
+
 // Host copies into and out of the pinned staging memory, with non-temporal
 // (streaming) stores: the data is not read again by this CPU (the DMA engine
 // reads the arena; the caller reads its output later), so write-allocate reads
@@ -34,7 +75,6 @@ using kern::ApplyParams;
 // the data is handed on.
 void stream_copy(uint8_t* dst, const uint8_t* src, size_t n)
 {
-#ifndef AB_NO_STREAM_COPY
     if (n >= 4096) {
         const size_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
         std::memcpy(dst, src, head);
@@ -56,7 +96,6 @@ void stream_copy(uint8_t* dst, const uint8_t* src, size_t n)
         src += body;
         n -= body;
     }
-#endif
     std::memcpy(dst, src, n);
 }
 
@@ -188,6 +227,7 @@ public:
     {
         for (int s = 0; s < kSlots; ++s) {
             if (stream_[s]) (void)hipStreamDestroy(stream_[s]);
+            if (ev_[s]) (void)hipEventDestroy(ev_[s]);
             if (pin_in_[s]) (void)hipHostFree(pin_in_[s]);
             if (pin_out_[s]) (void)hipHostFree(pin_out_[s]);
             if (d_in_[s]) (void)hipFree(d_in_[s]);
@@ -207,7 +247,7 @@ public:
         if (op.hashes) {  // every chunk's kernel adds into d_hash_; start from 31^len
             hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_hash_),
                                              static_cast<int>(kern::pow31(len)), op.rows, stream_[0]);
-            if (e == hipSuccess) e = hipStreamSynchronize(stream_[0]);
+            if (e == hipSuccess) e = wait_stream(stream_[0], ev_[0]);
             if (e != hipSuccess) return map_hip(e);
         }
         size_t pending[kSlots] = {};
@@ -215,7 +255,7 @@ public:
         for (size_t c = 0; c < nchunks + kSlots; ++c) {
             const int s = static_cast<int>(c % kSlots);
             if (busy[s]) {  // retire the chunk that used this slot
-                const hipError_t e = hipStreamSynchronize(stream_[s]);
+                const hipError_t e = wait_stream(stream_[s], ev_[s]);
                 if (e != hipSuccess) return map_hip(e);
                 const size_t o = pending[s] * step;
                 const size_t n = std::min(step, len - o);
@@ -247,8 +287,8 @@ public:
             if (e == hipSuccess)
                 e = hipMemcpyAsync(pin_out_[s], d_out_[s], op.rows * pitch, hipMemcpyDeviceToHost, stream_[s]);
             if (e != hipSuccess) {
-                (void)hipStreamSynchronize(stream_[0]);
-                (void)hipStreamSynchronize(stream_[1]);
+                (void)wait_stream(stream_[0], ev_[0]);
+                (void)wait_stream(stream_[1], ev_[1]);
                 return map_hip(e);
             }
             pending[s] = c;
@@ -290,7 +330,8 @@ private:
     {
         if (!stream_[0]) {
             for (int s = 0; s < kSlots; ++s) {
-                const hipError_t e = hipStreamCreateWithFlags(&stream_[s], hipStreamNonBlocking);
+                hipError_t e = hipStreamCreateWithFlags(&stream_[s], hipStreamNonBlocking);
+                if (e == hipSuccess) e = make_wait_event(&ev_[s]);
                 if (e != hipSuccess) return map_hip(e);
             }
             hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_hash_), kern::kMaxRows * sizeof(int32_t));
@@ -333,6 +374,7 @@ private:
 
     int dev_;
     hipStream_t stream_[kSlots] = {};
+    hipEvent_t ev_[kSlots] = {};  // blocking waits on the slots' streams (wait_stream)
     uint8_t* pin_in_[kSlots] = {};
     uint8_t* pin_out_[kSlots] = {};
     uint8_t* d_in_[kSlots] = {};
@@ -512,8 +554,11 @@ public:
                 return kFallback;
             }
             try {
-                std::thread(&Batcher::worker, this).detach();  // lives as long as the process
+                // the completion thread first: a dispatcher without it would strand its batches
+                if (wait_mode() != WaitMode::kCallback) std::thread(&Batcher::completer, this).detach();
+                std::thread(&Batcher::worker, this).detach();  // both live as long as the process
             } catch (...) {  // no dispatcher: the per-thread engine serves every call
+                // (a completion thread that did start only ever waits for batches that never come)
                 release();
                 init_failed_ = true;
                 return kFallback;
@@ -612,6 +657,7 @@ private:
         std::condition_variable done;  // this batch's callers wait here for kDone
         hipStream_t stream = nullptr;
         hipEvent_t h2d_done = nullptr;
+        hipEvent_t done_ev = nullptr;  // recorded behind the batch's D2H (the completion thread waits on it)
 
         Shape shape() const
         {
@@ -663,7 +709,8 @@ private:
         for (Slab& s : active()) {
             s.owner = this;
             hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming);
+            if (e == hipSuccess) e = make_wait_event(&s.h2d_done);
+            if (e == hipSuccess) e = make_wait_event(&s.done_ev);
             // device first: an arena too large for the device fails there, before any host pinning
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_in), arena);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_out), arena);
@@ -687,6 +734,7 @@ private:
         for (Slab& s : active()) {
             if (s.stream) (void)hipStreamDestroy(s.stream);
             if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
+            if (s.done_ev) (void)hipEventDestroy(s.done_ev);
             for (uint8_t* h : {s.pin_in, s.pin_out})
                 if (h) (void)hipHostFree(h);
             for (void* h : {static_cast<void*>(s.pin_lens), static_cast<void*>(s.pin_hash)})
@@ -696,6 +744,7 @@ private:
                 if (d) (void)hipFree(d);
             s.stream = nullptr;
             s.h2d_done = nullptr;
+            s.done_ev = nullptr;
             s.pin_in = s.pin_out = s.d_in = s.d_out = nullptr;
             s.pin_lens = s.d_lens = nullptr;
             s.pin_hash = s.d_hash = nullptr;
@@ -738,9 +787,14 @@ private:
             const int n = s->reserved;
             lock.unlock();
             const hipError_t e = issue(*s, shape, n);
-            if (e != hipSuccess) (void)hipStreamSynchronize(s->stream);  // no callback was queued
+            if (e != hipSuccess) (void)hipStreamSynchronize(s->stream);  // no completion was queued
             lock.lock();
-            if (e != hipSuccess) finish(s, map_hip(e));
+            if (e != hipSuccess) {
+                finish(s, map_hip(e));
+            } else if (wait_mode() != WaitMode::kCallback) {
+                completing_.push_back(s);
+                cv_complete_.notify_one();
+            }
             prev = s;
         }
     }
@@ -789,8 +843,30 @@ private:
         if (e == hipSuccess && sh.hashed)
             e = hipMemcpyAsync(s.pin_hash, s.d_hash, static_cast<size_t>(n) * sh.rows * sizeof(int32_t),
                                hipMemcpyDeviceToHost, s.stream);
-        if (e == hipSuccess) e = hipLaunchHostFunc(s.stream, &Batcher::on_done, &s);
+        if (e == hipSuccess)
+            e = wait_mode() == WaitMode::kCallback ? hipLaunchHostFunc(s.stream, &Batcher::on_done, &s)
+                                                   : hipEventRecord(s.done_ev, s.stream);
         return e;
+    }
+
+    // Completion thread (block and spin modes): waits for the issued batches in
+    // issue order, each on the event behind its D2H, and hands every batch back
+    // to its callers.  With blocking events it sleeps while the device works; a
+    // host-function callback (callback mode) is run by a HIP runtime thread
+    // that polls instead.
+    void completer()
+    {
+        (void)hipSetDevice(dev_);
+        std::unique_lock<std::mutex> lock(mu_);
+        for (;;) {
+            cv_complete_.wait(lock, [&] { return !completing_.empty(); });
+            Slab* s = completing_.front();
+            completing_.pop_front();
+            lock.unlock();
+            const hipError_t e = hipEventSynchronize(s->done_ev);
+            lock.lock();
+            finish(s, map_hip(e));
+        }
     }
 
     static void on_done(void* arg)  // HIP host-function callback: no HIP calls in here
@@ -820,6 +896,8 @@ private:
     std::mutex mu_;
     std::condition_variable cv_worker_;  // the dispatcher
     std::condition_variable cv_slot_;    // callers waiting for an arena to reserve in
+    std::condition_variable cv_complete_;  // the completion thread
+    std::deque<Slab*> completing_;         // issued batches, in issue order (under mu_)
     bool started_ = false;
     bool init_failed_ = false;  // the arenas could not be allocated: every call runs directly
     size_t arena_ = 0;
@@ -882,7 +960,20 @@ struct ZeroCopy {
         return m == 2 || (len >= kMinBytes && in_flight <= kMaxInFlight && alone);
     }
 
-    // Page-aligned, merged [begin, end) intervals covering every unit of the call.
+    // Bytes of input j the kernels may touch: a padded unit's content rounded up
+    // to the 16-byte segment, never past the unit.  The padded vector kernel
+    // loads the whole segment that holds a content end (rs_impl.hpp,
+    // gf_apply_x16<PAD>) and masks it: up to 15 bytes past lens[j], which on a
+    // caller pointer off 16-byte alignment can cross into a page registered for
+    // nothing.  So those bytes are registered too.
+    static size_t input_span(const HostOp& op, int j, size_t len)
+    {
+        if (!op.lens) return len;
+        return std::min(len, (op.lens[j] + 15) & ~size_t{15});
+    }
+
+    // Page-aligned, merged [begin, end) intervals covering every byte the
+    // call's kernels touch.
     static std::vector<std::pair<uintptr_t, uintptr_t>> ranges(const HostOp& op, size_t len)
     {
         constexpr uintptr_t kPage = 4096;
@@ -892,7 +983,7 @@ struct ZeroCopy {
             const uintptr_t a = reinterpret_cast<uintptr_t>(p);
             r.emplace_back(a & ~(kPage - 1), (a + n + kPage - 1) & ~(kPage - 1));
         };
-        for (int j = 0; j < op.cols; ++j) add(op.in[j], op.lens ? op.lens[j] : len);
+        for (int j = 0; j < op.cols; ++j) add(op.in[j], input_span(op, j, len));
         for (int q = 0; q < op.rows; ++q) add(op.out[q], len);
         std::sort(r.begin(), r.end());
         std::vector<std::pair<uintptr_t, uintptr_t>> m;
@@ -905,16 +996,41 @@ struct ZeroCopy {
         return m;
     }
 
+    // This thread's stream and wait event per device, destroyed when the thread
+    // exits (ELECT's coding pools retire threads).
+    struct ThreadStreams {
+        hipStream_t stream[kMaxDevices] = {};
+        hipEvent_t done[kMaxDevices] = {};
+        ~ThreadStreams()
+        {
+            for (int d = 0; d < kMaxDevices; ++d) {
+                if (!stream[d] && !done[d]) continue;
+                int prev = 0;
+                const bool other = hipGetDevice(&prev) == hipSuccess && prev != d && hipSetDevice(d) == hipSuccess;
+                if (done[d]) (void)hipEventDestroy(done[d]);
+                if (stream[d]) (void)hipStreamDestroy(stream[d]);
+                if (other) (void)hipSetDevice(prev);
+            }
+        }
+    };
+
     static int run(const HostOp& op, size_t len)
     {
-        thread_local hipStream_t streams[kMaxDevices] = {};
+        thread_local ThreadStreams ts;
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return kFallback;
-        if (!streams[dev] && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess) {
-            streams[dev] = nullptr;
-            (void)hipGetLastError();
-            return kFallback;
+        if (!ts.stream[dev]) {
+            if (hipStreamCreateWithFlags(&ts.stream[dev], hipStreamNonBlocking) != hipSuccess) {
+                ts.stream[dev] = nullptr;
+                (void)hipGetLastError();
+                return kFallback;
+            }
+            if (make_wait_event(&ts.done[dev]) != hipSuccess) {
+                ts.done[dev] = nullptr;  // wait_stream then synchronizes the stream itself
+                (void)hipGetLastError();
+            }
         }
+        hipStream_t stream = ts.stream[dev];
         const auto rs = ranges(op, len);
         size_t locked = 0;
         for (; locked < rs.size(); ++locked)
@@ -943,12 +1059,19 @@ struct ZeroCopy {
             }
             if (op.lens) {  // one stripe: the per-column content lengths ride in the kernel arguments
                 p.padded = true;
-                for (int j = 0; j < op.cols; ++j) p.clen[j] = static_cast<uint32_t>(op.lens[j]);
+                for (int j = 0; j < op.cols; ++j) p.clen[j] = static_cast<uint32_t>(std::min(op.lens[j], len));
             }
             if (ok) {
-                hipError_t e = kern::launch_apply(p, streams[dev]);
-                if (e == hipSuccess) e = hipStreamSynchronize(streams[dev]);
-                rc = map_hip(e);  // a launch or fault error is the call's error: the outputs may be partial
+                hipError_t e = kern::launch_apply(p, stream);
+                // Whatever was enqueued finishes before the pages are unregistered,
+                // also when a later launch of the call failed.
+                const hipError_t w = wait_stream(stream, ts.done[dev]);
+                if (e == hipSuccess) e = w;
+                // A shape the single launch does not take (hipErrorInvalidValue is
+                // returned before the kernels run: a wide padded update past 2^31
+                // bytes, say) goes to the staged path, which splits it; the outputs
+                // are rewritten there in full.  Any other error is the call's.
+                rc = e == hipErrorInvalidValue ? kFallback : map_hip(e);
             }
         }
         for (size_t i = 0; i < locked; ++i) (void)hipHostUnregister(reinterpret_cast<void*>(rs[i].first));

@@ -411,12 +411,10 @@ template <int K, int R, bool MASKED = false>
 __device__ __forceinline__ void gf_combine(const uint4 (&x)[K], const uint32_t* tl, uint4 (&acc)[R],
                                            uint32_t cmask = ~0u)
 {
-#ifndef AB_COMBINE1
     if constexpr (!MASKED) {
         gf_combine_pairs<K, R>(x, tl, acc);
         return;
     }
-#endif
     if (MASKED) {
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
@@ -569,17 +567,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
             const uint32_t q = kLanePow.v[threadIdx.x & 63u] * p0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-#if defined(AB_HASH_NOSUM)  // timing probes only (wrong hashes): no wave reduction / no Horner
-                const uint32_t sum = horner31(acc[r]) * q;
-#elif defined(AB_HASH_NOHORNER)
-                const uint32_t sum = wave_sum(acc[r].x * q);
-#elif defined(AB_HASH_ROWSUM)  // row sums only (4 DPP steps, no row broadcasts)
-                uint32_t v = horner31(acc[r]) * q;
-                v = dpp_add<0xB1>(v); v = dpp_add<0x4E>(v); v = dpp_add<0x124>(v); v = dpp_add<0x128>(v);
-                const uint32_t sum = v;
-#else
                 const uint32_t sum = wave_sum(horner31(acc[r]) * q);
-#endif
                 if ((threadIdx.x & 63u) == 0) a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum;
             }
         } else if (a.hpart_hi) {  // assign mode: a wave straddling two stripes (or the launch's end)
@@ -652,29 +640,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16u(const FastArgs<K, R> a)
 // masked, so no byte loads.  Straddling waves take a one-segment-at-a-time path.
 constexpr int kAuxNT = 2;  // buffer op cache policy: nt (gfx940 family CPol)
 
-// HASH (add mode only: entries seeded with 31^len by launch_apply): a wave
-// inside one stripe sums its U*64 segments' hash terms in registers (constant
-// 31^(1024u) weights per slice) and writes ONE partial per row, into the slot
-// of its first 64-segment group, zeros into its other U-1 slots (hash_reduce
-// adds the slots of every group wholly inside a stripe); a straddling wave
-// zeroes its slots and adds per lane atomically.  So the wave reduction is paid
-// once per U KiB per column instead of once per KiB (gf_apply_x16<.., HASH>).
-template <int U>
-struct SlicePow {  // 31^(16*64*u), u < U
-    uint32_t v[U];
-    constexpr SlicePow() : v()
-    {
-        uint32_t p = 1;
-        for (int i = 0; i < 1024; ++i) p *= 31u;
-        uint32_t x = 1;
-        for (int u = 0; u < U; ++u) {
-            v[u] = x;
-            x *= p;
-        }
-    }
-};
-
-template <int K, int R, int U, bool HASH>
+template <int K, int R, int U>
 __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
@@ -720,9 +686,6 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
                 if (off0 < sl[j] && sl[j] < off0 + 1024u && (sl[j] & 15u))  // wave-uniform: this slice holds the content end
                     x[u][j] = keep_bytes(x[u][j], off < sl[j] ? min(sl[j] - off, 16u) : 0u);
         }
-        uint32_t hacc[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) hacc[r] = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t idx = first + u * 64u + lane;
@@ -739,39 +702,8 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
             gf_combine<K, R, true>(x[u], tl, acc, cmask);
 #pragma unroll
             for (int r = 0; r < R; ++r) store_nt(a.dp[r] + s0 * a.ds[r] + off, acc[r]);
-            if constexpr (HASH) {
-                constexpr SlicePow<U> kSlice{};
-#pragma unroll
-                for (int r = 0; r < R; ++r) hacc[r] += u == 0 ? horner31(acc[r]) : horner31(acc[r]) * kSlice.v[u];
-            }
-        }
-        if constexpr (HASH) {
-            if (a.hashes) {  // the whole wave again (the slice loop may have left early)
-                const uint32_t hs = div_magic(first, a.hmagic, a.hshift);
-                const uint32_t q = kLanePow.v[lane] * (a.hpow * pow31_seg(first - hs * a.hsegs));
-                const uint64_t slot = first >> 6;
-                // hash_reduce reads only 64-segment groups wholly inside the launch: a
-                // wave reaching its end adds per lane instead (lanes past it hold 0)
-                const bool tail = first + 64u * U > a.total;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    if (tail) {
-                        if (hacc[r]) atomicAdd(reinterpret_cast<unsigned*>(a.hashes) + static_cast<uint64_t>(hs) * a.hstride + r,
-                                               hacc[r] * q);
-                        if (lane < U && first + 64u * lane < a.total) a.hpart[(slot + lane) * R + r] = 0u;
-                        continue;
-                    }
-                    const uint32_t sum = wave_sum(hacc[r] * q);
-                    if (lane < U) a.hpart[(slot + lane) * R + r] = lane == 0 ? sum : 0u;
-                }
-            }
         }
         return;
-    }
-    if (HASH && a.hashes) {  // straddling wave: its slots read as zero, terms added per lane below
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (lane < U && first + 64u * lane < a.total) a.hpart[((first >> 6) + lane) * R + r] = 0u;
     }
     for (int u = 0; u < U; ++u) {  // straddling wave: per-lane stripes and lengths
         const uint32_t idx = first + u * 64u + lane;
@@ -793,14 +725,6 @@ __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
         gf_combine<K, R>(x, tl, acc);
 #pragma unroll
         for (int r = 0; r < R; ++r) store_nt(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
-        if (HASH && a.hashes) {
-            const uint32_t hs = div_magic(idx, a.hmagic, a.hshift);
-            const uint32_t p = a.hpow * pow31_seg(idx - hs * a.hsegs);
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                atomicAdd(reinterpret_cast<unsigned*>(a.hashes) + static_cast<uint64_t>(hs) * a.hstride + r,
-                          horner31(acc[r]) * p);
-        }
     }
 }
 
@@ -857,113 +781,13 @@ __global__ __launch_bounds__(kBlock) void gf_apply_group(const GroupArgs<K, R> a
     for (int r = 0; r < R; ++r) store_nt(g.dp[r] + stripe * g.ds[r] + off, acc[r]);
 }
 
-// Plain launches with U segments per lane (A/B: AB_PLAIN_U > 1): a wave codes
-// U adjacent 1 KiB slices per column, all U*K loads issued before any compute,
-// so a wave keeps U times the bytes in flight at the same occupancy cap.
-template <int K, int R, int U>
-__global__ __launch_bounds__(kBlock) void gf_apply_x16m(const FastArgs<K, R> a)
-{
-    __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t first = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * (64u * U);
-    stage_tables<K, R>(a.tab, tl);
-    if (__builtin_amdgcn_readfirstlane(first) >= a.total) return;
-    uint4 x[U][K];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint32_t idx = min(first + u * 64u + lane, a.total - 1);  // past the end: redo the last segment
-        const uint32_t stripe = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
-        const uint64_t off = static_cast<uint64_t>(idx - stripe * a.segs) * 16;
-#pragma unroll
-        for (int j = 0; j < K; ++j) x[u][j] = load_nt(a.sp[j] + stripe * a.ss[j] + off);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint32_t idx = first + u * 64u + lane;
-        if (idx >= a.total) break;
-        const uint32_t stripe = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
-        const uint64_t off = static_cast<uint64_t>(idx - stripe * a.segs) * 16;
-        uint4 acc[R];
-        gf_combine<K, R>(x[u], tl, acc);
-#pragma unroll
-        for (int r = 0; r < R; ++r) store_nt(a.dp[r] + stripe * a.ds[r] + off, acc[r]);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Persistent forms of the plain and grouped kernels: one resident wave of
-// workgroups (grid = CUs x the blocks the occupancy cap lets each CU hold),
-// each staging the tables ONCE and then walking the launch's blocks in a
-// grid stride (virtual block b = blockIdx.x, + gridDim.x, ...).  Every
-// virtual block codes exactly the segments the ordinary launch's block b
-// would, so bytes, order of HBM windows and results are unchanged; what goes
-// is the per-block wave launch and table staging (kernarg loads, LDS writes,
-// a barrier) on the critical path of every 1 KiB per column.  No block waits
-// on another: each loop ends when its next virtual block is past the launch.
-// ---------------------------------------------------------------------------
-template <int K, int R, bool UNI>
-__global__ __launch_bounds__(kBlock) void gf_apply_x16p(const FastArgs<K, R> a, uint32_t vblocks)
-{
-    __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
-    stage_tables<K, R>(a.tab, tl);
-    for (uint32_t b = blockIdx.x; b < vblocks; b += gridDim.x) {
-        const uint32_t idx = b * blockDim.x + threadIdx.x;
-        if (idx >= a.total) break;  // (UNI: whole waves; later blocks lie further past the end)
-        uint32_t stripe;
-        uint64_t off;
-        if constexpr (UNI) {
-            stripe = div_magic(__builtin_amdgcn_readfirstlane(idx), a.magic, a.shift);
-            off = static_cast<uint32_t>((idx - stripe * a.segs) * 16u);
-        } else {
-            stripe = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
-            off = static_cast<uint64_t>(idx - stripe * a.segs) * 16;
-        }
-        uint4 x[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + static_cast<uint64_t>(stripe) * a.ss[j] + off);
-        uint4 acc[R];
-        gf_combine<K, R>(x, tl, acc);
-#pragma unroll
-        for (int r = 0; r < R; ++r) store_nt(a.dp[r] + static_cast<uint64_t>(stripe) * a.ds[r] + off, acc[r]);
-    }
-}
-
-template <int K, int R, bool UNI>
-__global__ __launch_bounds__(kBlock) void gf_apply_groupp(const GroupArgs<K, R> a, uint32_t vblocks)
-{
-    __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
-    stage_tables<K, R>(a.tab, tl);
-    for (uint32_t b = blockIdx.x; b < vblocks; b += gridDim.x) {
-        int p = 0;
-        for (int q = 1; q < a.n; ++q)
-            if (b >= a.part[q].block0) p = q;
-        const GroupPart<K, R>& g = a.part[p];
-        const uint32_t idx = (b - g.block0) * blockDim.x + threadIdx.x;
-        if (idx >= g.total) continue;  // the part's last block may be partial; later blocks are other parts
-        const uint32_t stripe = UNI ? div_magic(__builtin_amdgcn_readfirstlane(idx), g.magic, g.shift)
-                                    : static_cast<uint32_t>((static_cast<uint64_t>(idx) * g.magic) >> g.shift);
-        const uint64_t off = UNI ? static_cast<uint64_t>(static_cast<uint32_t>((idx - stripe * g.segs) * 16u))
-                                 : static_cast<uint64_t>(idx - stripe * g.segs) * 16;
-        uint4 x[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) x[j] = load_nt(g.sp[j] + stripe * g.ss[j] + off);
-        uint4 acc[R];
-        gf_combine<K, R>(x, tl, acc);
-#pragma unroll
-        for (int r = 0; r < R; ++r) store_nt(g.dp[r] + stripe * g.ds[r] + off, acc[r]);
-    }
-}
-
-#ifndef AB_PAD_U4
-#define AB_PAD_U4 2
-#endif
 // Segments per lane for gf_apply_lens: U*K 16-byte loads in flight per lane.
 // U = 2 since round 3 (3 interleaved rounds, profiles/r03/padded_and_plain_u_ab.txt):
 // ELECT's degraded read 77.3 -> 81.6 % of peak at 64 KiB codeLength and 80.7 ->
 // 82.2 % at 4.4 MB in 64 KiB tiles, padded encode at 93 % fill 79.1 -> 80.1 %,
 // full units 81.0 -> 82.3 %, random fill 69.1 -> 68.8 % (noise); U = 4 before.
 template <int K>
-constexpr int lens_unroll() { return K <= 4 ? AB_PAD_U4 : 1; }
+constexpr int lens_unroll() { return K <= 4 ? 2 : 1; }
 
 // Sum the per-wave hash partials of each (stripe, row); one wave per pair:
 // lanes stride over the partials, then a wave sum; lane 0 is the sole writer.
@@ -999,177 +823,123 @@ constexpr int lens_unroll() { return K <= 4 ? AB_PAD_U4 : 1; }
     }
 }
 
-// Block size by shape (the occupancy caps below are set per block size; the
-// per-family choices since round 3 are in DESIGN.md §4, launch shape table):
-// small chunks (<= 4 KiB per shard) run 128-thread blocks (3-4 % over 256 in
-// round 1; one-wave blocks measured the same in round 3), launches of >= 16
-// coefficients 128 (read-heavy) or 256 (write-heavy), and plain launches of
-// fewer coefficients one-wave blocks (plain_one_wave, below).  Keeping the
-// tables in SGPRs instead of LDS (no barrier) lost 1 % on RS(6,4).
-#ifndef AB_BLOCK_WIDE_READ  // A/B: read-heavy launches of >= 16 coefficients (RS(12,8) decodes)
-#define AB_BLOCK_WIDE_READ 128
-#endif
-// Write-heavy ones (RS(12,8) encodes) run 256-thread blocks since the occupancy
-// caps (round 3, 3 interleaved rounds, profiles/r03/block_wide_ab.txt): 64 /
-// 128 / 256 threads 75.5 / 73.9 / 76.8 % of peak; read-heavy ones keep 128
-// (64: the same within noise; 256: 78 % against 85 %).
-#ifndef AB_BLOCK_WIDE_WRITE  // A/B: write-heavy launches of >= 16 coefficients (RS(12,8) encodes)
-#define AB_BLOCK_WIDE_WRITE 256
-#endif
-#ifndef AB_WAVES_HASH_PAD  // A/B: occupancy cap of padded launches with the parity hash (0: uncapped)
-#define AB_WAVES_HASH_PAD 0
-#endif
-#ifndef AB_BLOCK_PAD_WRITE  // A/B: block size of unhashed padded write-heavy launches
-#define AB_BLOCK_PAD_WRITE 128
-#endif
-#ifndef AB_BLOCK_HASH_PAD  // A/B: block size of padded launches with the parity hash
-#define AB_BLOCK_HASH_PAD 64
-#endif
-#ifdef AB_BLOCK  // A/B builds (tools/ab_build.sh): one block size for every launch
-inline int block_for(uint64_t, int, int) { return AB_BLOCK; }
+// ---------------------------------------------------------------------------
+// Launch policy: the block size and the occupancy cap of every launch.
+//
+// The cap is the number of the launch's waves resident per CU (0: uncapped),
+// set with dynamic LDS that no block reads (cap_lds: 160 KiB per CU / blocks).
+// Fewer waves in flight keep fewer HBM pages open: an uncapped RS(6,4) decode
+// waits on DRAM read credits 6x as often (profiles/r02_pmc_occupancy_ab.txt).
+// One-wave blocks let the cap move in single waves; the best points (18 waves
+// for RS(6,4), 12 for RS(12,8) decodes) lie two waves above cliffs where the
+// rate falls by several points.  Every entry was chosen by interleaved A/B
+// runs of the product library; the evidence file is named beside it, and
+// DESIGN.md §4 has the launch-shape table.  A/B builds swap the whole table
+// (tools/ab_build.sh NAME -DELECT_EC_POLICY_HEADER='"file.hpp"'); the product
+// compiles this one.
+// ---------------------------------------------------------------------------
+struct LaunchPolicy {
+    // Plain launches (no padding, no hash): gf_apply_x16 / gf_apply_x16u.
+    uint64_t small_len = 4096;       // chunks up to this run 128-thread blocks (round 1: +3-4 % over 256)
+    int small_block = 128;
+    // > 4 KiB and < 16 coefficients: one-wave blocks (profiles/r03/plain_one_wave_ab.txt: RS(6,4)
+    // encode 82.5 -> 84.1 %, decode 81.6 -> 83.8 %, RS(12,8) one-erasure decode 79.0 -> 84.8 %)
+    int one_wave_write_waves = 18;   // write-heavy (2R >= K): RS(6,4) encode (14: 82.0 %, 12: 75.7 %)
+    int one_wave_read_waves = 18;    // read-heavy, < 8 columns: RS(6,4) decode (15: 80.7 %)
+    int one_wave_read_wide_waves = 12;  // read-heavy, >= 8 columns: RS(12,8) one-erasure decode
+    // >= 16 coefficients, and chunks <= 4 KiB
+    int wide_write_block = 256;      // RS(12,8) encode: 64 / 128 / 256 threads 75.5 / 73.9 / 76.8 % (block_wide_ab.txt)
+    int wide_read_block = 128;       // RS(12,8) decodes (64: the same; 256: 78 against 85 %)
+    int write_waves = 24;            // profiles/r02_occupancy_ab/ (RS(12,8) encode at 16 / 12: 72.5 / 66.9 %)
+    int read_waves = 20;             // profiles/r02_occupancy_ab/ (1 KiB decodes at 16 / 24: 80.7 / 81.4 vs 82.4 %)
+    int read_wide_waves = 12;        // >= 8 columns and >= 2 rows: RS(12,8) two-erasure decode at 20 / 16 / 14 /
+                                     // 12 / 10 waves 78.2 / 79.5 / 83.0 / 85.2 / 75.7 % (occupancy_wide_ab.txt)
+    // Plain launches with the parity hash (the fused-hash encode): one-wave blocks;
+    // the scalar-base form capped at 20 waves (80.7 -> 81.2 %, plain_one_wave_ab.txt),
+    // the per-lane form uncapped (caps of 24 / 28 cost 5 / 3 points, profiles/r02_hash_ab/)
+    int hashed_block = 64;
+    int hashed_scalar_waves = 20;
+    // Padded launches: gf_apply_x16<PAD> (uncapped) and gf_apply_lens (capped).
+    int padded_write_block = 128;    // random fill 68.9 -> 71.8 %, full 82.3 -> 82.7 % (block_pad_ab.txt);
+                                     // read-heavy ones keep the plain block (64 / 128: -3 / -4 points)
+    int lens_write_waves = 24;       // gf_apply_lens: degraded read 76.4 -> 77.4 % at 20 (profiles/r02_lenscap_ab/)
+    int lens_read_waves = 20;
+    // Padded launches with the hash (ELECT's fused encode and update steps): one-wave
+    // blocks, uncapped (79.6 -> 81.0 % at ELECT's codeLength; caps of 20-28 lose:
+    // block_hash_pad_ab.txt)
+    int padded_hashed_block = 64;
+    // Grouped launches (the mixed config): one-wave blocks with the plain caps of their
+    // shape (8-way share 4,198 -> 4,397 GiB/s; group_small_block_ab.txt, plain_one_wave_ab.txt)
+    int group_block = 64;
+    // The parity update gf_update_x16: 81.6 -> 84.2 % (plain_one_wave_ab.txt)
+    int update_block = 64;
+    int update_waves = 18;
+    // Scalar stripe bases (gf_apply_x16u, the grouped kernel's UNI form) for plain launches
+    // of whole-wave stripes with at least this many columns: RS(12,8) two-erasure decode
+    // 79.9 -> 81.6 %; four-column shapes lose 0.5 % with them (profiles/r02_scalarbase_ab/)
+    int scalar_base_min_cols = 8;
+};
+
+#ifdef ELECT_EC_POLICY_HEADER
+#include ELECT_EC_POLICY_HEADER  // defines kPolicy (A/B builds only)
 #else
-inline int block_for(uint64_t len, int cols, int rows)
-{
-    if (len <= 4096) return 128;
-    if (cols * rows >= 16) return 2 * rows >= cols ? AB_BLOCK_WIDE_WRITE : AB_BLOCK_WIDE_READ;
-    return kBlock;
-}
+constexpr LaunchPolicy kPolicy{};
 #endif
+
+struct LaunchShape {
+    int block;
+    int waves;  // resident waves per CU, 0 = uncapped
+};
+
+enum class Family {
+    kPlain,         // gf_apply_x16 / gf_apply_x16u
+    kPlainHashed,   // the same with the parity-hash epilogue
+    kPadded,        // gf_apply_x16<PAD> (one length per column, or L % 16 != 0)
+    kLens,          // gf_apply_lens (per-stripe content lengths, tiles)
+    kPaddedHashed,  // gf_apply_x16<PAD, HASH>
+    kGroup,         // gf_apply_group
+    kUpdate,        // gf_update_x16
+};
+
+// The shape of a launch of `cols` source columns and `rows` output rows over
+// `len`-byte chunks; scalar_base: the scalar-base form (gf_apply_x16u).
+inline LaunchShape launch_shape(Family f, int cols, int rows, uint64_t len, bool scalar_base = false)
+{
+    const LaunchPolicy& P = kPolicy;
+    const bool write_heavy = 2 * rows >= cols;
+    const bool wide = cols * rows >= 16;
+    // the plain caps for blocks of more than one wave
+    const int multi_cap = write_heavy ? P.write_waves : (cols >= 8 && rows >= 2) ? P.read_wide_waves : P.read_waves;
+    const int one_wave_cap = write_heavy ? P.one_wave_write_waves
+                             : cols >= 8 ? P.one_wave_read_wide_waves
+                                         : P.one_wave_read_waves;
+    // the plain block of a shape: 128 for small chunks, 256 / 128 for wide shapes, else 256
+    const int plain_block = len <= P.small_len ? P.small_block
+                            : wide            ? (write_heavy ? P.wide_write_block : P.wide_read_block)
+                                              : kBlock;
+    switch (f) {
+    case Family::kPlain:
+        if (len > P.small_len && !wide) return {64, one_wave_cap};
+        return {plain_block, multi_cap};
+    case Family::kPlainHashed: return {P.hashed_block, scalar_base ? P.hashed_scalar_waves : 0};
+    case Family::kPadded:
+    case Family::kLens: {
+        const int block = write_heavy ? std::min(P.padded_write_block, plain_block) : plain_block;
+        if (f == Family::kPadded) return {block, 0};
+        return {block, write_heavy ? P.lens_write_waves : P.lens_read_waves};
+    }
+    case Family::kPaddedHashed: return {P.padded_hashed_block, 0};
+    case Family::kGroup: return {P.group_block, !wide ? one_wave_cap : multi_cap};
+    case Family::kUpdate: return {P.update_block, P.update_waves};
+    }
+    return {kBlock, 0};
+}
 
 constexpr int kMaxHashCols = 10;  // ELECT_EC_MAX_DATA_UNITS: hashed launches are encodes
-
-// Occupancy cap for the plain streaming kernel (gf_apply_x16 without padding
-// or hash): dynamic LDS that no block reads, so that at most `waves` waves of a
-// launch are resident per CU (160 KiB of LDS per CU / blocks).  Fewer waves in
-// flight keep fewer HBM pages open at once.  Measured (occupancy
-// sweep, 3 interleaved rounds): uncapped (32 waves) -> 20 waves: RS(6,4) decode
-// 77.3 -> 81.0 % of peak, the mixed config +3 %, RS(12,8) decode 77 -> 80 %;
-// encodes (R >= K/2: more writes in flight) peak at 24.  PMC: the uncapped
-// decode waits on DRAM read credits 6x as often (profiles/r02_pmc_occupancy_ab.txt).
-// The hashed and update kernels lost with any cap (the hash epilogue wants the
-// waves: ELECT's fused steps 80 -> 67 % at 20) and run uncapped.
-#ifndef AB_WAVES_READ_HEAVY
-#define AB_WAVES_READ_HEAVY 20
-#endif
-#ifndef AB_WAVES_WRITE_HEAVY
-#define AB_WAVES_WRITE_HEAVY 24
-#endif
-// Read-heavy launches of 8 or more source columns (RS(12,8) decodes) keep twice
-// the read streams open per wave: 12 waves per CU there (round 3, interleaved
-// rounds on two boxes, profiles/r03/occupancy_wide_ab.txt): RS(12,8)
-// two-erasure decode at 20 / 16 / 14 / 12 / 10 / 8 waves 78.2 / 79.5 / 83.0 /
-// 85.2 / 75.7 / 75.7 % of peak (configs[4] 4,541 -> 4,935 GiB/s at 12, alone;
-// 4,458-4,489 -> 4,765-4,775 inside the headline line), three erasures 79.1 ->
-// 82.2 %; one erasure (8 coefficients, 256-thread blocks) keeps 20 (77.7 % at
-// 12 against 78.1 %); 16 for every read-heavy shape cost the mixed config's
-// 1-4 KiB decodes 2-4 points.
-#ifndef AB_WAVES_READ_HEAVY_WIDE
-#define AB_WAVES_READ_HEAVY_WIDE 12
-#endif
-// (write-heavy ones of 8 or more columns keep 24: RS(12,8) encode at 16 / 12
-// waves 72.5 / 66.9 % against 74.6 %)
-// Plain launches (no padding, no hash) of chunks above 4 KiB and fewer than 16
-// coefficients run one-wave blocks, their cap set in single waves: RS(6,4)
-// encode at 16 waves per CU 82.4-82.6 -> 83.6-84.2 % of peak (14: 82.0, 12:
-// 75.7 %), RS(6,4) single-erasure decode at 17-18 waves 80.8-82.0 -> 83.8-84.1 %
-// (15: 80.7 %), RS(12,8) single-erasure decode at 12 waves 78.8-79.0 -> 84.8-85.0 %
-// (profiles/r03/plain_one_wave_ab.txt).  Finer block steps place the cap where
-// 256-thread blocks (4 waves a step) cannot.  Padded, hashed and grouped
-// launches keep their own shapes (padded decodes and full-size groups lose with
-// one-wave blocks).
-#ifndef AB_PLAIN_ONE_WAVE  // A/B: 0 = off
-#define AB_PLAIN_ONE_WAVE 1
-#endif
-#ifndef AB_WAVES_PLAIN_WRITE
-#define AB_WAVES_PLAIN_WRITE 18
-#endif
-#ifndef AB_WAVES_PLAIN_READ
-#define AB_WAVES_PLAIN_READ 18
-#endif
-#ifndef AB_WAVES_PLAIN_READ_WIDE
-#define AB_WAVES_PLAIN_READ_WIDE 12
-#endif
-// Unpadded hashed launches (the fused-hash encode) run one-wave blocks at 20
-// waves per CU: 80.7 -> 81.2 % of peak (one-wave uncapped 80.4, at 24 waves
-// 81.0 %; profiles/r03/plain_one_wave_ab.txt).  Unhashed padded encodes keep
-// 128-thread blocks: one-wave ones at 16-20 waves gain at ELECT's fill (93 %:
-// 80.4 -> 82.1 %) but lose at random fill (71.9 -> 69.5 %).
-#ifndef AB_BLOCK_HASH_PLAIN  // A/B: block size of unpadded hashed launches (0: block_for)
-#define AB_BLOCK_HASH_PLAIN 64
-#endif
-#ifndef AB_WAVES_HASH_PLAIN  // A/B: their occupancy cap (0: uncapped)
-#define AB_WAVES_HASH_PLAIN 20
-#endif
-#ifndef AB_PAD_READ_ONE_WAVE  // A/B: padded read-heavy launches in one-wave blocks at this cap (0 = off)
-#define AB_PAD_READ_ONE_WAVE 0
-#endif
-#ifndef AB_PLAIN_ONE_WAVE_SMALL  // A/B: chunks <= 4 KiB too (1 = on)
-#define AB_PLAIN_ONE_WAVE_SMALL 0
-#endif
-// Grouped launches of one-wave blocks (short groups, kSmallGroupBytes) take the
-// one-wave caps too: the mixed config's 8-way share 4,272 -> 4,397 GiB/s
-// (profiles/r03/plain_one_wave_ab.txt).  Chunks <= 4 KiB keep 128-thread blocks
-// (one-wave blocks there: 1 KiB encode -0.6, decode +1 point, the same value).
-#ifndef AB_GROUP_ONE_WAVE_CAPS  // A/B: 0 = the caps of plain_waves_cap
-#define AB_GROUP_ONE_WAVE_CAPS 1
-#endif
-inline bool plain_one_wave(uint64_t len, int cols, int rows)
-{
-    return AB_PLAIN_ONE_WAVE && (len > 4096 || AB_PLAIN_ONE_WAVE_SMALL) && cols * rows < 16;
-}
-inline int plain_one_wave_cap(int cols, int rows)
-{
-    if (2 * rows >= cols) return AB_WAVES_PLAIN_WRITE;
-    return cols >= 8 ? AB_WAVES_PLAIN_READ_WIDE : AB_WAVES_PLAIN_READ;
-}
-#ifndef AB_WAVES_WRITE_HEAVY_WIDE  // A/B: write-heavy launches of 8 or more source columns (RS(12,8) encodes)
-#define AB_WAVES_WRITE_HEAVY_WIDE AB_WAVES_WRITE_HEAVY
-#endif
 constexpr size_t kLdsPerCU = 160 * 1024;
-#ifndef AB_PERSIST  // A/B builds only (tools/ab_build.sh NAME -DAB_PERSIST=1): compile the persistent
-#define AB_PERSIST 0   // kernels, chosen at run time by ELECT_EC_PERSIST; measured slower
-#endif
-#ifndef AB_PLAIN_U  // A/B: segments per lane of plain (per-lane addressed) launches; 1 = gf_apply_x16
-#define AB_PLAIN_U 1
-#endif
-#ifndef AB_PLAIN_U_MAX_R  // ... for launches of at most this many output rows (1: decodes only)
-#define AB_PLAIN_U_MAX_R 4
-#endif
-#ifndef AB_PLAIN_U_WAVES  // ... and this occupancy cap (0: plain_waves_cap)
-#define AB_PLAIN_U_WAVES 0
-#endif
 
-// (and narrow read-heavy ones of 128-thread blocks, chunks <= 4 KiB, keep 20 too:
-// 1 KiB decodes at 16 / 24 waves 80.7 / 81.4 % against 82.4 %; write-heavy wide
-// ones at 28 / 32 waves measured the same as 24)
-#ifndef AB_WAVES_READ_HEAVY_SMALL  // A/B: narrow read-heavy launches of 128-thread blocks (chunks <= 4 KiB)
-#define AB_WAVES_READ_HEAVY_SMALL AB_WAVES_READ_HEAVY
-#endif
-
-inline int plain_waves_cap(int cols, int rows, int block)
-{
-    if (2 * rows >= cols) return cols >= 8 ? AB_WAVES_WRITE_HEAVY_WIDE : AB_WAVES_WRITE_HEAVY;
-    if (cols >= 8 && rows >= 2) return AB_WAVES_READ_HEAVY_WIDE;  // (>= 16 coefficients: 128-thread blocks)
-    return block < kBlock ? AB_WAVES_READ_HEAVY_SMALL : AB_WAVES_READ_HEAVY;
-}
-
-inline size_t cap_lds(int block, int coefs, int waves);
-
-// The padded per-stripe-length kernel takes the same cap: 64 KiB degraded-read
-// decode (flows) 76.4 -> 77.4 %, padded encodes unchanged (3 interleaved rounds).
-#ifndef AB_CAP_LENS
-#define AB_CAP_LENS 1
-#endif
-#ifndef AB_WAVES_PAD_WRITE  // A/B: occupancy cap of padded write-heavy launches (per-stripe lengths)
-#define AB_WAVES_PAD_WRITE AB_WAVES_WRITE_HEAVY
-#endif
-inline size_t lens_cap(int block, int coefs, int cols, int rows)
-{
-    // (the wide caps above were measured on the plain kernels only)
-    const int waves = 2 * rows >= cols ? AB_WAVES_PAD_WRITE : (AB_PAD_READ_ONE_WAVE ? AB_PAD_READ_ONE_WAVE : AB_WAVES_READ_HEAVY);
-    return AB_CAP_LENS ? cap_lds(block, coefs, AB_CAP_LENS > 1 ? AB_CAP_LENS : waves) : 0;
-}
-
+// Dynamic LDS that caps a launch of `block`-thread blocks at `waves` resident
+// waves per CU (0: none).  The block's static LDS (its coefficient tables) counts.
 inline size_t cap_lds(int block, int coefs, int waves)
 {
     if (waves <= 0) return 0;
@@ -1179,88 +949,17 @@ inline size_t cap_lds(int block, int coefs, int waves)
     return per_block > static_lds ? per_block - static_lds : 0;
 }
 
-// Persistent launches (gf_apply_x16p / gf_apply_groupp), in AB_PERSIST builds only:
-// ELECT_EC_PERSIST = 0 (off), 1 (plain and grouped launches) or 2 (grouped only); read once.
-inline int persist_mode()
-{
-    if constexpr (AB_PERSIST == 0) return 0;
-    static const int m = [] {
-        const char* e = std::getenv("ELECT_EC_PERSIST");
-        return e ? std::atoi(e) : 0;
-    }();
-    return m;
-}
-
-// Compute units of the current device (cached per device).
-inline int device_cus()
-{
-    static std::mutex mu;
-    static int cus[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    std::lock_guard<std::mutex> lock(mu);
-    if (!cus[dev]) {
-        int n = 0;
-        cus[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
-    }
-    return cus[dev];
-}
-
-// Grid of a persistent launch: every CU holds `waves` waves (the occupancy cap)
-// of `block`-thread blocks, at most the launch's own block count.
-inline uint32_t persist_grid(uint64_t vblocks, int block, int waves)
-{
-    const uint64_t per_cu = static_cast<uint64_t>(std::max(1, waves / (block / 64)));
-    return static_cast<uint32_t>(std::min<uint64_t>(vblocks, per_cu * static_cast<uint64_t>(device_cus())));
-}
+inline size_t cap_lds(const LaunchShape& sh, int coefs) { return cap_lds(sh.block, coefs, sh.waves); }
 
 // Padded launches the per-stripe-length kernel can take (whole 16-byte segments,
-// aligned columns).  Hashed ones with per-stripe content lengths, untiled, of at
-// most 4 columns take it too, 2 segments per lane, in add mode only (launch_apply_impl
-// seeds the entries for them).  Interleaved A/B against gf_apply_x16<.., HASH>
-// (profiles/r02_lenshash_ab/): ELECT's fused steps at 64 KiB codeLength, encode
-// 73.1 -> 74.2 %, update 74.6 -> 76.0 %; but ELECT's 4.4 MB codeLength in tiles lost
-// 2 points (79.5 -> 77.6 %), full hashed units 1 % (3,762 -> 3,725 GiB/s), and
-// 4 segments per lane (121 VGPRs) or 1 lost everywhere: those stay on gf_apply_x16.
-// Round 3: with one-wave blocks for padded hashed launches (AB_BLOCK_HASH_PAD) the
-// one-segment gf_apply_x16<.., PAD, HASH> beats it at 64 KiB codeLength too:
-// encode 76.0 -> 78.1 %, update 76.7 -> 78.5 % (U = 1 / 4 in one-wave blocks:
-// 72.6 / 73.5 % encode; profiles/r03/lens_hash_ab.txt), so the path is off.
-#ifndef AB_LENS_HASH
-#define AB_LENS_HASH 0
-#endif
-#ifndef AB_LENS_HASH_U
-#define AB_LENS_HASH_U 2
-#endif
-#ifndef AB_LENS_HASH_MIN_LEN  // A/B knob: the lens path only at or above this unit length
-#define AB_LENS_HASH_MIN_LEN 0
-#endif
+// aligned columns).  (Hashed launches do not: a hashed form of gf_apply_lens
+// gained 1 point at 64 KiB codeLength in round 2 and lost to the one-segment
+// hashed kernel in one-wave blocks in round 3, profiles/r03/lens_hash_ab.txt;
+// it was removed in round 4, its source is in git history before that.)
 inline bool lens_eligible(const ApplyParams& p)
 {
     return p.aligned16 && p.len % 16 == 0 && p.len > 0 && p.len < (uint64_t{1} << 31);
 }
-
-inline bool lens_hash_path(const ApplyParams& p)
-{
-    return AB_LENS_HASH && p.hashes && p.padded && p.lens && p.tiles <= 1 && p.cols <= 4 &&
-           p.len >= AB_LENS_HASH_MIN_LEN && lens_eligible(p);
-}
-
-// gf_apply_x16u (and the grouped kernel's UNI form) for plain launches of
-// whole-wave stripes with at least this many columns.  Interleaved A/B
-// (profiles/r02_scalarbase_ab/): RS(12,8) two-erasure decode (K = 8) 79.9 ->
-// 81.6 % of peak, 4,618 -> 4,716 GiB/s; RS(6,4) encode 82.7 -> 82.2 %, its
-// decode +0.5, the mixed config -0.5 %: the four-column shapes keep the
-// per-lane addressing.  AB builds: -DAB_SCALAR_BASE_MIN_K=99 turns it off.
-#ifndef AB_SCALAR_BASE_MIN_K
-#define AB_SCALAR_BASE_MIN_K 8
-#endif
-#ifndef AB_SCALAR_BASE_R1  // A/B: single-row plain launches (one-erasure decodes) of any width too
-#define AB_SCALAR_BASE_R1 0
-#endif
-#ifndef AB_SCALAR_BASE_HASH  // hashed plain launches of whole-wave stripes, any width
-#define AB_SCALAR_BASE_HASH 1
-#endif
 
 template <int K, int R, bool PAD>
 hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
@@ -1295,23 +994,11 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     a.hpow = pow31(p.hash_base);
     for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(p.coef[(r0 + r) * p.cols + j]);
-    // Padded launches with the parity hash (ELECT's fused encode and update steps)
-    // run one-wave blocks: the fused encode step 80.0 -> 81.4 % of peak at ELECT's
-    // codeLength (64 KiB tiles) and 74.7 -> 76.3 % at 64 KiB codeLength, the
-    // update step unchanged (round 3, profiles/r03/block_hash_pad_ab.txt).
-    // Unhashed padded encodes (per-unit content lengths) run 128-thread blocks:
-    // 64 KiB units at random fill 70.2 -> 73.8 % of peak, at ELECT's fill (93 %)
-    // 80.2 -> 80.7 %, full 82.1 -> 82.4 %; padded decodes keep 256 (64 / 128 threads:
-    // -3 / -4 points) (profiles/r03/block_pad_ab.txt).
-    const bool one_wave = !PAD && !p.hashes && plain_one_wave(p.len, K, R);
-    const bool pad_read_one_wave = AB_PAD_READ_ONE_WAVE && PAD && !p.hashes && 2 * R < K;
-    const int block = one_wave || pad_read_one_wave ? 64
-                      : PAD && p.hashes ? AB_BLOCK_HASH_PAD
-                      : PAD && 2 * R >= K ? std::min(AB_BLOCK_PAD_WRITE, block_for(p.len, K, R))
-                      : !PAD && p.hashes && AB_BLOCK_HASH_PLAIN ? AB_BLOCK_HASH_PLAIN
-                                          : block_for(p.len, K, R);
-    const int plain_cap = one_wave ? plain_one_wave_cap(K, R) : plain_waves_cap(K, R, block);
     const bool hash_assign = p.hashes && p.hash_seed;  // launch_apply chose assign mode
+    // scalar stripe bases: plain launches of whole-wave stripes (kPolicy.scalar_base_min_cols
+    // columns and up; hashed ones of any width)
+    const bool whole_waves = !PAD && a.segs % 64 == 0 && segs64 < (uint64_t{1} << 28);
+    const bool scalar_base = whole_waves && (p.hashes ? K <= kMaxHashCols : K >= kPolicy.scalar_base_min_cols);
     // stripes per launch keeping idx < 2^31, whole logical stripes (tiles) per launch
     const uint64_t per_launch = kMaxIndex / segs64 / tiles * tiles;
     for (uint64_t s0 = 0; s0 < p.stripes; s0 += per_launch) {
@@ -1335,76 +1022,41 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             a.hpart = p.hash_scratch;
             if (hash_assign) a.hpart_hi = a.hpart + n;
         }
-        bool lens_path = false;
+        constexpr int kCoefs = R * K;
         if constexpr (PAD) {
-            lens_path = a.hashes ? lens_hash_path(p) && !hash_assign : (a.lens || tiles > 1) && lens_eligible(p);
-#ifdef AB_NO_LENS
-            lens_path = false;
-#endif
-            if (lens_path) {
+            if (!a.hashes && (a.lens || tiles > 1) && lens_eligible(p)) {
                 constexpr int U = lens_unroll<K>();
+                const LaunchShape sh = launch_shape(Family::kLens, K, R, p.len);
                 const uint64_t threads = (static_cast<uint64_t>(a.total) + 64 * U - 1) / (64 * U) * 64;
-                const dim3 grid(static_cast<uint32_t>((threads + block - 1) / block));
-                if (!a.hashes)
-                    hipLaunchKernelGGL((gf_apply_lens<K, R, U, false>), grid, dim3(block), lens_cap(block, R * K, K, R),
-                                       stream, a);
-                else if constexpr (K <= 4) {  // (lens_hash_path)
-                    constexpr int UH = AB_LENS_HASH_U;
-                    const uint64_t th = (static_cast<uint64_t>(a.total) + 64 * UH - 1) / (64 * UH) * 64;
-                    hipLaunchKernelGGL((gf_apply_lens<K, R, UH, true>), dim3(static_cast<uint32_t>((th + block - 1) / block)),
-                                       dim3(block), cap_lds(block, R * K, AB_WAVES_HASH_PAD), stream, a);
-                }
+                hipLaunchKernelGGL((gf_apply_lens<K, R, U>), dim3(static_cast<uint32_t>((threads + sh.block - 1) / sh.block)),
+                                   dim3(sh.block), cap_lds(sh, kCoefs), stream, a);
+            } else if (!a.hashes) {
+                const LaunchShape sh = launch_shape(Family::kPadded, K, R, p.len);
+                hipLaunchKernelGGL((gf_apply_x16<K, R, true, false>), dim3((a.total + sh.block - 1) / sh.block),
+                                   dim3(sh.block), cap_lds(sh, kCoefs), stream, a);
+            } else if constexpr (K <= kMaxHashCols) {
+                const LaunchShape sh = launch_shape(Family::kPaddedHashed, K, R, p.len);
+                hipLaunchKernelGGL((gf_apply_x16<K, R, true, true>), dim3((a.total + sh.block - 1) / sh.block),
+                                   dim3(sh.block), cap_lds(sh, kCoefs), stream, a);
             }
-        }
-        if (!lens_path) {
-            const uint32_t grid = (a.total + block - 1) / block;
-            bool scalar_base = false;
-            constexpr bool kPlainU = K >= AB_SCALAR_BASE_MIN_K || (AB_SCALAR_BASE_R1 && R == 1);
-            if constexpr (!PAD)
-                scalar_base = (a.hashes ? AB_SCALAR_BASE_HASH != 0 && K <= kMaxHashCols : kPlainU) &&
-                              a.segs % 64 == 0 && segs64 < (uint64_t{1} << 28);
-            if (AB_PLAIN_U > 1 && !PAD && !a.hashes && !scalar_base && R <= AB_PLAIN_U_MAX_R) {  // A/B: U per lane
-                if constexpr (!PAD && AB_PLAIN_U > 1) {
-                    constexpr int U = AB_PLAIN_U;
-                    const uint64_t th = (static_cast<uint64_t>(a.total) + 64 * U - 1) / (64 * U) * 64;
-                    hipLaunchKernelGGL((gf_apply_x16m<K, R, U>), dim3(static_cast<uint32_t>((th + block - 1) / block)),
-                                       dim3(block), cap_lds(block, R * K, AB_PLAIN_U_WAVES ? AB_PLAIN_U_WAVES : plain_cap),
-                                       stream, a);
-                }
-            } else if (AB_PERSIST && !PAD && !a.hashes && persist_mode() == 1) {  // persistent form (gf_apply_x16p)
-                if constexpr (!PAD && AB_PERSIST != 0) {
-                    const int waves = plain_cap;
-                    const dim3 pg(persist_grid(grid, block, waves));
-                    const size_t lds = cap_lds(block, R * K, waves);
-                    if constexpr (kPlainU) {
-                        if (scalar_base)
-                            hipLaunchKernelGGL((gf_apply_x16p<K, R, true>), pg, dim3(block), lds, stream, a, grid);
-                        else
-                            hipLaunchKernelGGL((gf_apply_x16p<K, R, false>), pg, dim3(block), lds, stream, a, grid);
-                    } else {
-                        hipLaunchKernelGGL((gf_apply_x16p<K, R, false>), pg, dim3(block), lds, stream, a, grid);
+        } else {
+            const LaunchShape sh = launch_shape(a.hashes ? Family::kPlainHashed : Family::kPlain, K, R, p.len, scalar_base);
+            const dim3 grid((a.total + sh.block - 1) / sh.block);
+            const size_t lds = cap_lds(sh, kCoefs);
+            if (!a.hashes) {
+                bool launched = false;
+                if constexpr (K >= kPolicy.scalar_base_min_cols) {  // (scalar-base plain instances: wide shapes only)
+                    if (scalar_base) {
+                        hipLaunchKernelGGL((gf_apply_x16u<K, R, false>), grid, dim3(sh.block), lds, stream, a);
+                        launched = true;
                     }
                 }
-            } else if (scalar_base) {
-                if constexpr (!PAD && kPlainU) {
-                    if (!a.hashes)
-                        hipLaunchKernelGGL((gf_apply_x16u<K, R, false>), dim3(grid), dim3(block),
-                                           cap_lds(block, R * K, plain_cap), stream, a);
-                }
-                if constexpr (!PAD && K <= kMaxHashCols) {
-                    if (a.hashes)
-                        hipLaunchKernelGGL((gf_apply_x16u<K, R, true>), dim3(grid), dim3(block),
-                                           cap_lds(block, R * K, AB_WAVES_HASH_PLAIN), stream, a);
-                }
-            } else if (!a.hashes) {
-                hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, false>), dim3(grid), dim3(block),
-                                   PAD ? 0 : cap_lds(block, R * K, plain_cap), stream, a);
+                if (!launched) hipLaunchKernelGGL((gf_apply_x16<K, R, false, false>), grid, dim3(sh.block), lds, stream, a);
             } else if constexpr (K <= kMaxHashCols) {
-                // (uncapped: capping the hashed instance at 24 / 28 waves per CU cost it 5 / 3
-                // points, and staging 31^(16*lane) in LDS instead of constant memory gained
-                // nothing; profiles/r02_hash_ab/)
-                hipLaunchKernelGGL((gf_apply_x16<K, R, PAD, true>), dim3(grid), dim3(block),
-                                   PAD ? cap_lds(block, R * K, AB_WAVES_HASH_PAD) : 0, stream, a);
+                if (scalar_base)
+                    hipLaunchKernelGGL((gf_apply_x16u<K, R, true>), grid, dim3(sh.block), lds, stream, a);
+                else
+                    hipLaunchKernelGGL((gf_apply_x16<K, R, false, true>), grid, dim3(sh.block), lds, stream, a);
             }  // (launch_apply rejects hashed launches wider than kMaxHashCols)
         }
         hipError_t e = hipGetLastError();
@@ -1428,23 +1080,11 @@ constexpr std::array<FastFn, kFastRows> fast_row_fns()
 }
 
 // Grouped launches take every groupable batch of a call, whatever its chunk
-// size, in one launch of the smallest block size any part wants (block_for):
-// the mixed config's 8-way share 3,879 -> 3,959 GiB/s, 4-way 4,084 -> 4,116,
-// full size unchanged, against one launch per block-size class; one launch of
-// 256-thread blocks lost 5 % at full size (profiles/r02_group_ab/).
-// A/B builds: -DAB_GROUP_BLOCK=-1 restores one launch per class, 128 / 256 force a size.
-#ifndef AB_GROUP_BLOCK
-#define AB_GROUP_BLOCK 0
-#endif
-#ifndef AB_GROUP_SMALL_BLOCK  // A/B: block size of grouped launches under kSmallGroupBytes of source (kBlock: off)
-#define AB_GROUP_SMALL_BLOCK 64
-#endif
-#ifndef AB_SMALL_GROUP_BYTES  // A/B: groups of at least this many source bytes keep the larger blocks
-#define AB_SMALL_GROUP_BYTES (~uint64_t{0})
-#endif
-constexpr uint64_t kSmallGroupBytes = AB_SMALL_GROUP_BYTES;
-inline int group_class(const ApplyParams& p) { return AB_GROUP_BLOCK < 0 ? block_for(p.len, p.cols, std::min(p.rows, kFastRows)) : 0; }
-
+// size, in one launch (the mixed config's 8-way share 3,879 -> 3,959 GiB/s
+// against one launch per block-size class, profiles/r02_group_ab/), of one-wave
+// blocks with the plain caps of the shape (round 3: 8-way share 4,272 -> 4,397,
+// 4-way 4,312 -> 4,461, 2-way 4,488 -> 4,568, full size 4,461 -> 4,531 GiB/s,
+// profiles/r03/plain_one_wave_ab.txt).
 // Launch parts [0, n) of a group (all plain, vector-capable, whole segments,
 // same coefficients) for output rows r0 .. r0+R-1.
 template <int K, int R>
@@ -1454,25 +1094,10 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
     a.n = n;
     for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(ps[0].coef[(r0 + r) * ps[0].cols + j]);
-    int block = kBlock;
-    bool uni = true;  // (used for K >= AB_SCALAR_BASE_MIN_K)
-    uint64_t bytes = 0;  // source bytes of the launch
-    for (int i = 0; i < n; ++i) {
-        block = std::min(block, block_for(ps[i].len, K, R));
-        uni = uni && (ps[i].len / 16) % 64 == 0 && ps[i].len < (uint64_t{1} << 32);
-        bytes += ps[i].len * ps[i].stripes * K;
-    }
-    // Grouped launches run one-wave blocks with the one-wave caps of the plain
-    // launches.  With round 2's caps one-wave blocks won only for short groups
-    // (the mixed config's 8-way share: 4,198 -> 4,276 GiB/s; the 4-way share and
-    // full size lost, profiles/r03/group_small_block_ab.txt); with the one-wave
-    // caps they win at every size: 8-way share 4,272 -> 4,397, 4-way 4,312 ->
-    // 4,461, 2-way 4,488 -> 4,568, full size 4,461 -> 4,531 GiB/s
-    // (profiles/r03/plain_one_wave_ab.txt).
-    if (bytes < kSmallGroupBytes) block = std::min(block, AB_GROUP_SMALL_BLOCK);
-    if (AB_GROUP_BLOCK > 0) block = AB_GROUP_BLOCK;
-    const int group_cap = AB_GROUP_ONE_WAVE_CAPS && block == 64 && K * R < 16 ? plain_one_wave_cap(K, R)
-                                                                              : plain_waves_cap(K, R, block);
+    bool uni = true;  // every part's stripes hold whole waves: scalar stripe bases
+    for (int i = 0; i < n; ++i) uni = uni && (ps[i].len / 16) % 64 == 0 && ps[i].len < (uint64_t{1} << 32);
+    const LaunchShape sh = launch_shape(Family::kGroup, K, R, ps[0].len);
+    const int block = sh.block;
     uint64_t blocks = 0;
     for (int i = 0; i < n; ++i) {
         const ApplyParams& p = ps[i];
@@ -1495,34 +1120,13 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
         blocks += (g.total + block - 1) / block;
     }
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    if constexpr (AB_PERSIST != 0) {
-        if (persist_mode() >= 1) {  // persistent form (gf_apply_groupp)
-            const int waves = group_cap;
-            const dim3 pg(persist_grid(blocks, block, waves));
-            const size_t lds = cap_lds(block, R * K, waves);
-            const uint32_t vb = static_cast<uint32_t>(blocks);
-            if constexpr (K >= AB_SCALAR_BASE_MIN_K) {
-                if (uni) {
-                    hipLaunchKernelGGL((gf_apply_groupp<K, R, true>), pg, dim3(block), lds, stream, a, vb);
-                    return hipGetLastError();
-                }
-            }
-            hipLaunchKernelGGL((gf_apply_groupp<K, R, false>), pg, dim3(block), lds, stream, a, vb);
-            return hipGetLastError();
-        }
-    }
-    if constexpr (K >= AB_SCALAR_BASE_MIN_K) {
-        if (uni) {
-            hipLaunchKernelGGL((gf_apply_group<K, R, true>), dim3(static_cast<uint32_t>(blocks)), dim3(block),
-                               cap_lds(block, R * K, group_cap), stream, a);
-            return hipGetLastError();
-        }
-    }
-    hipLaunchKernelGGL((gf_apply_group<K, R, false>), dim3(static_cast<uint32_t>(blocks)), dim3(block),
-                       cap_lds(block, R * K, group_cap), stream, a);
+    const size_t lds = cap_lds(sh, R * K);
+    if (uni && K >= kPolicy.scalar_base_min_cols)
+        hipLaunchKernelGGL((gf_apply_group<K, R, true>), dim3(static_cast<uint32_t>(blocks)), dim3(block), lds, stream, a);
+    else
+        hipLaunchKernelGGL((gf_apply_group<K, R, false>), dim3(static_cast<uint32_t>(blocks)), dim3(block), lds, stream, a);
     return hipGetLastError();
 }
-
 
 template <int K>
 constexpr std::array<GroupFn, kFastRows> group_row_fns()

@@ -233,16 +233,9 @@ hipError_t launch_bytes(const ApplyParams& p, hipStream_t stream)
 // Parity update: par_out[r] = par_in[r] ^ c_r * (old ^ new), fused.
 // ---------------------------------------------------------------------------
 // The plain parity update runs one-wave blocks, 18 waves per CU, like the plain
-// encodes: 81.6 -> 84.2 % of peak (uncapped 256-thread blocks before; caps on
-// those, 20-28 waves, measured within noise; one-wave blocks at 16 / 22 waves:
-// 83.5 / 83.8 %; profiles/r03/plain_one_wave_ab.txt).
-#ifndef AB_WAVES_UPDATE  // A/B: occupancy cap of the plain parity update (0: uncapped)
-#define AB_WAVES_UPDATE 18
-#endif
-#ifndef AB_BLOCK_UPDATE  // A/B: its block size
-#define AB_BLOCK_UPDATE 64
-#endif
-
+// encodes (kPolicy.update_*): 81.6 -> 84.2 % of peak (uncapped 256-thread blocks
+// before; caps on those, 20-28 waves, measured within noise; one-wave blocks at
+// 16 / 22 waves: 83.5 / 83.8 %; profiles/r03/plain_one_wave_ab.txt).
 template <int R>
 struct UpdArgs {
     const uint8_t* op;
@@ -307,9 +300,9 @@ hipError_t launch_update_r(const UpdateParams& p, int r0, hipStream_t stream)
             a.pos[r] = p.par_out[r0 + r].stride;
         }
         a.total = static_cast<uint32_t>(ns * segs64);
-        const uint32_t grid = (a.total + AB_BLOCK_UPDATE - 1) / AB_BLOCK_UPDATE;
-        hipLaunchKernelGGL((gf_update_x16<R>), dim3(grid), dim3(AB_BLOCK_UPDATE),
-                           cap_lds(AB_BLOCK_UPDATE, 0, AB_WAVES_UPDATE), stream, a);
+        const LaunchShape sh = launch_shape(Family::kUpdate, 2, R, p.len);
+        const uint32_t grid = (a.total + sh.block - 1) / sh.block;
+        hipLaunchKernelGGL((gf_update_x16<R>), dim3(grid), dim3(sh.block), cap_lds(sh, 0), stream, a);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -403,6 +396,46 @@ bool unaligned_vector_ok()
     return state[dev] == 1;
 }
 
+// HBM ceilings measured with the same access instructions as the coding
+// kernels (bench.py reports the coding kernels against them).
+template <int KIND>
+__global__ __launch_bounds__(kBlock) void hbm_probe_kernel(const uint8_t* in, uint8_t* out, uint64_t segs)
+{
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= segs) return;
+    if constexpr (KIND == 0) {
+        const uint4 v = load_nt(in + i * 16);
+        // never true for the probe's data; keeps the load live (a per-lane vector store)
+        if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9E3779B9u) reinterpret_cast<uint32_t*>(out)[threadIdx.x & 63u] = 1;
+    } else if constexpr (KIND == 1) {
+        store_nt(out + i * 16, make_uint4(static_cast<uint32_t>(i), 1u, 2u, 3u));
+    } else {
+        store_nt(out + i * 16, load_nt(in + i * 16));
+    }
+}
+
+hipError_t hbm_probe(int kind, const void* src, void* dst, size_t bytes, int block, int waves, hipStream_t stream)
+{
+    (void)hipGetLastError();
+    if (kind < 0 || kind > 2 || bytes % 16 || (block != 64 && block != 128 && block != 256) || waves < 0 || !dst ||
+        (kind != 1 && !src))
+        return hipErrorInvalidValue;
+    const uint64_t segs = bytes / 16;
+    const uint64_t grid = (segs + block - 1) / block;
+    if (grid == 0) return hipSuccess;
+    if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    const auto* in = static_cast<const uint8_t*>(src);
+    auto* out = static_cast<uint8_t*>(dst);
+    const size_t lds = cap_lds(block, 0, waves);
+    if (kind == 0)
+        hipLaunchKernelGGL(hbm_probe_kernel<0>, dim3(static_cast<uint32_t>(grid)), dim3(block), lds, stream, in, out, segs);
+    else if (kind == 1)
+        hipLaunchKernelGGL(hbm_probe_kernel<1>, dim3(static_cast<uint32_t>(grid)), dim3(block), lds, stream, in, out, segs);
+    else
+        hipLaunchKernelGGL(hbm_probe_kernel<2>, dim3(static_cast<uint32_t>(grid)), dim3(block), lds, stream, in, out, segs);
+    return hipGetLastError();
+}
+
 bool apply_is_aligned(const ApplyParams& p)
 {
     for (int j = 0; j < p.cols; ++j)
@@ -437,7 +470,7 @@ hipError_t launch_apply_impl(const ApplyParams& p_in, hipStream_t stream)
         // unit (every wave within two units); anything else seeds the entries and adds.
         const bool fast = vec && (!p.padded || p.cols <= kMaxPadCols) && !wide_hash;
         const uint64_t segs = (p.padded ? (p.len + 15) / 16 : p.len / 16) * tiles;
-        if (!fast || segs < 64 || lens_hash_path(p)) {
+        if (!fast || segs < 64) {
             const hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.hashes), static_cast<int>(pow31(ulen)),
                                                    p.stripes / tiles * p.hash_stride, stream);
             if (e != hipSuccess) return e;
@@ -508,16 +541,9 @@ hipError_t launch_apply_many(const ApplyParams* ps, int n, hipStream_t stream)
         const hipError_t e = launch_apply_impl(p, stream);
         if (e != hipSuccess) return e;
     }
-    // Batches group in submission order (group_class: one class unless an A/B build
-    // splits them by block size).
-    std::stable_sort(grouped.begin(), grouped.end(), [](const ApplyParams& x, const ApplyParams& y) {
-        return group_class(x) < group_class(y);
-    });
+    // Batches group in submission order, kMaxGroup per launch.
     for (size_t g0 = 0; g0 < grouped.size();) {
-        const int cls = group_class(grouped[g0]);
-        size_t g1 = g0 + 1;
-        while (g1 < grouped.size() && g1 - g0 < kMaxGroup && group_class(grouped[g1]) == cls)
-            ++g1;
+        const size_t g1 = std::min(grouped.size(), g0 + kMaxGroup);
         const int m = static_cast<int>(g1 - g0);
         if (m == 1) {  // nothing to group with: the plain launcher
             const hipError_t e = launch_apply_impl(grouped[g0], stream);

@@ -132,5 +132,12 @@ bool apply_is_aligned(const ApplyParams& p);
 // layouts run the dwordx4 kernels too; otherwise the byte-granular kernel.
 bool unaligned_vector_ok();
 
+// HBM ceiling probes (diagnostics, elect_ec_hbm_probe): one 16-byte segment per
+// lane with the kernels' non-temporal loads/stores, `block`-thread blocks, at
+// most `waves` waves per CU (0: uncapped).  kind 0: read `bytes` of src (dst
+// takes one dword per lane of a wave whose data hits a magic value: at least
+// 256 bytes); 1: write `bytes` of dst; 2: copy src -> dst.
+hipError_t hbm_probe(int kind, const void* src, void* dst, size_t bytes, int block, int waves, hipStream_t stream);
+
 }  // namespace kern
 }  // namespace elect

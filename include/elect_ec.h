@@ -82,6 +82,17 @@ int elect_ec_device_count(int* count);
  * run the vector kernels on the calling thread's current device; 0 when they
  * fall back to the byte-granular kernel.  Checked once per device. */
 int elect_ec_unaligned_vector_ok(int* ok);
+/* Diagnostics: the HBM ceilings the coding kernels are measured against
+ * (bench.py's roofline).  Enqueues one probe kernel on `stream` (a hipStream_t,
+ * NULL = the null stream) of the current device: 16 bytes per lane with the
+ * coding kernels' non-temporal loads and stores, `block` = 64, 128 or 256
+ * threads, at most waves_per_cu resident waves per CU (0: uncapped).
+ * kind 0: read `bytes` of src (dst: a device buffer of >= 256 bytes that is
+ * written only if the data hits a magic value); 1: write `bytes` of dst;
+ * 2: copy `bytes` from src to dst.  bytes % 16 == 0.  No reference
+ * counterpart: ELECT has no device path. */
+int elect_ec_hbm_probe(int kind, const void* src, void* dst, size_t bytes, int block, int waves_per_cu,
+                       void* stream);
 
 /* Devices for the host-memory calls.  By default a calling thread uses its
  * current HIP device.  With a device list, each calling thread is assigned one

@@ -829,3 +829,38 @@ print("fanout ok")
     env = dict(__import__("os").environ, ELECT_EC_COPY_THREADS=helpers)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0 and "fanout ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_configs0_literal_every_byte(dev, oracle):
+    """BASELINE configs[0] as written: RS(6,4) encode of 1,000 random 64 KiB data
+    chunks (250 stripes of k = 4), every parity byte against the oracle, through
+    both boundaries ELECT has: the device batch (elect_ec_encode_batch) and the
+    JNI calling convention, one synchronous elect_ec_encode per stripe
+    (EC/NativeRSEncoder.c:43-61).  Then ErasureCodeTest's decode on every stripe
+    (ErasureCodeTest.java:89-109: erase {0}, decodeIndexes {4, 1, 2, 3}, inputs
+    [parity 0, data 1, data 2, data 3]), every rebuilt byte against the oracle's
+    decode and against the original chunk."""
+    from elect_amd.batch import decode_batch, encode_batch
+    from elect_amd.coder import RSCoder
+    k, m, L, B = 4, 2, 65536, 250
+    rng = np.random.default_rng(0xC0F160)
+    data = _rand(rng, B, k, L)  # 1,000 chunks
+    enc = oracle.Encoder(k, m)
+    want = np.stack([np.stack(enc.encode([data[s, j] for j in range(k)])) for s in range(B)])
+    c = RSCoder(k, m)
+    stripe = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
+    stripe[:, :k] = _to(dev, data)
+    encode_batch(c, stripe[:, :k], stripe[:, k:])
+    assert np.array_equal(stripe[:, k:].cpu().numpy(), want)
+    host_par = np.empty((B, m, L), np.uint8)
+    for s in range(B):
+        c.encode_host([data[s, j].ctypes.data for j in range(k)], [host_par[s, r].ctypes.data for r in range(m)], L)
+    assert np.array_equal(host_par, want)
+    surv = [4, 1, 2, 3]
+    out = torch.empty((B, 1, L), dtype=torch.uint8, device=dev)
+    decode_batch(c, stripe, surv, [0], out, inputs_by_unit=True)
+    got = out[:, 0].cpu().numpy()
+    for s in range(B):
+        rc, ref = oracle.decode(k, m, [want[s, 0], data[s, 1], data[s, 2], data[s, 3]], surv, [0])
+        assert rc == 0 and np.array_equal(got[s], ref[0]), s
+    assert np.array_equal(got, data[:, 0])

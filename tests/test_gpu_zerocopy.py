@@ -123,3 +123,64 @@ def test_zero_copy_falls_back_when_memory_is_already_locked():
 def test_zero_copy_off():
     st = _run({"ELECT_EC_ZEROCOPY": "0"}, [4404020], seed=10)
     assert st["zero_copy"] == 0 and st["zero_copy_fallback"] == 0 and st["batched"] == 6, st
+
+
+PAGE_EDGE = r"""
+import json, mmap, sys
+import numpy as np
+import torch
+sys.path.insert(0, ROOT)
+from elect_amd import _lib
+from elect_amd.coder import RSCoder
+from oracle import ec_oracle as orc
+
+torch.cuda.init()
+k, m, L, P = 4, 2, 65536, mmap.PAGESIZE
+rng = np.random.default_rng(11)
+maps = []
+
+def unit_at_plus8():
+    # an L-byte unit 8 bytes into its own page-aligned mapping (JNI inputOffsets do this)
+    mm = mmap.mmap(-1, L + 2 * P)
+    maps.append(mm)
+    a = np.frombuffer(mm, dtype=np.uint8)[8:8 + L]
+    a[:] = rng.integers(0, 256, L, dtype=np.uint8)
+    return a
+
+def zf(x, n):
+    return np.concatenate([x[:n], np.zeros(len(x) - n, np.uint8)])
+
+d = [unit_at_plus8() for _ in range(k)]
+# every content end lands exactly on a page boundary of its mapping: the segment that
+# holds it reaches 8 bytes into the next page, which only the content-rounded
+# registration covers
+lens = [t * P - 8 for t in (2, 3, 5, 16)]
+c = RSCoder(k, m)
+p = [np.zeros(L, np.uint8) for _ in range(m)]
+c.encode_ex_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L, data_lengths=lens)
+want = orc.Encoder(k, m).encode([zf(x, n) for x, n in zip(d, lens)])
+bad = [r for r in range(m) if not np.array_equal(p[r], want[r])]
+ins = [d[1], d[2], d[3], unit_at_plus8()]
+ins[3][:] = want[0]
+il = [lens[1], lens[2], lens[3], L]
+r = np.zeros(L, np.uint8)
+c.decode_ex_host([x.ctypes.data for x in ins], [1, 2, 3, 4], [0], [r.ctypes.data], L, input_lengths=il)
+wantd = orc.decode(k, m, [zf(x, n) for x, n in zip(ins, il)], [1, 2, 3, 4], [0])[1][0]
+if not np.array_equal(r, wantd):
+    bad.append("decode_ex")
+print("BAD" if bad else "OK", json.dumps(_lib.host_path_stats()))
+"""
+
+
+def test_zero_copy_content_end_on_page_boundary():
+    """A padded unit whose pointer is 8 bytes into a page and whose content ends
+    exactly on a page boundary: the padded kernel loads the whole segment holding
+    the content end (8 bytes past it), so the zero-copy registration must cover
+    the content rounded up to 16 bytes (host_path.cpp ZeroCopy::input_span)."""
+    code = PAGE_EDGE.replace("ROOT", repr(ROOT))
+    env = dict(os.environ, ELECT_EC_ZEROCOPY="2")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0 and r.stdout.strip().startswith("OK"), r.stdout[-2000:] + r.stderr[-2000:]
+    import json
+    st = json.loads(r.stdout.strip().split(" ", 1)[1])
+    assert st["zero_copy"] == 2 and st["zero_copy_fallback"] == 0, st

@@ -223,6 +223,29 @@ for step in "$@"; do
             run "rs12gap_inline_first_$i" 300 python bench.py --no-cpu --no-host --no-sizes --steps 20 --configs-order rs12,mixed || exit $?
             run "rs12gap_alone50_$i" 300 python bench.py --config rs12 || exit $?
         done ;;
+    sqpmc)  # what binds each shape: SQ issue/wait counters + DRAM stalls, one --pmc pass per set (round 4)
+        timeout -k 10 60 rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true
+        have() { local out=""; for c in "$@"; do b=${c%_sum}; grep -qw -- "$b" gpurun_out/counters_list.txt && out="$out $c"; done; echo $out; }
+        PA=$(have SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_LDS)
+        PB=$(have SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM)
+        PC=$(have TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum TCC_TOO_MANY_EA_WRREQS_STALL_sum)
+        echo "A: $PA"; echo "B: $PB"; echo "C: $PC"
+        for cfg in ${SQ_CFGS:-rs12 headline}; do
+            args="--config rs12 --steps 20 --warmup 3"
+            [ $cfg = headline ] && args="--no-cpu --no-host --no-sizes --no-configs --steps 20 --warmup 3"
+            [ $cfg = hashed ] && args="--config hashed --steps 20 --warmup 3"
+            for pass in A B C; do
+                ctr=$PA; [ $pass = B ] && ctr=$PB; [ $pass = C ] && ctr=$PC
+                [ -n "$ctr" ] || continue
+                run "sqpmc_${cfg}_$pass" 120 rocprofv3 --pmc $ctr GRBM_GUI_ACTIVE --kernel-trace --output-format csv \
+                    -d $OUT/sqpmc_${cfg}_$pass -o run -- python3 bench.py $args || exit $?
+            done
+        done ;;
+    hostwait)  # host-path waits: blocking events + completion thread / polling events / round 3's callbacks (round 4)
+        for i in 1 2; do for w in ${WAIT_MODES:-block spin callback}; do for T in ${WAIT_T:-1 16 64}; do
+            ELECT_EC_HOST_WAIT=$w run "hostwait_${w}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
+                --host-op ${HOST_OP:-encode} --host-seconds ${HOST_S:-2} || exit $?
+        done; done; done ;;
     padfill)  # padded encode vs content fill: where the time goes
         for f in 1.0 0.0 0.5 random; do
             run "bench_padded_fill_$f" 300 python bench.py --config padded --pad-fill $f || exit $?
