@@ -104,6 +104,10 @@ def parse():
                     help="hostpath: repeat the timed calls until at least this much wall time has passed")
     ap.add_argument("--no-hostpath", action="store_true",
                     help="headline: skip the JNI-convention host path over all the job's devices")
+    ap.add_argument("--host-alloc", choices=("pageable", "pinned"), default="pageable",
+                    help="hostpath: the callers' buffers are ordinary memory (ELECT's ByteBuffer.allocateDirect), or "
+                         "elect_ec_host_alloc buffers (page-locked; the batcher then moves them by DMA, no staging "
+                         "copies: INTEGRATION.md, host buffers)")
     ap.add_argument("--host-op", choices=("encode", "encode_ex"), default="encode",
                     help="hostpath: plain encode (the JNI encodeImpl), or ELECT's fused encode step "
                          "(encodeExImpl: content = codeLength/1.05, parity hashCodes)")
@@ -861,11 +865,26 @@ def config_hostpath(args, world, rank, dev):
         if ndev > avail:
             raise SystemExit(f"--host-devices {ndev}: only {avail} device(s) visible")
         _lib.set_host_devices(list(range(ndev)))
-    bufs = []
+    bufs, keep = [], []
+    pinned = args.host_alloc == "pinned"
+
+    def host_array(n):
+        if not pinned:
+            return np.empty(n, np.uint8)
+        hb = _lib.HostBuffer(n)  # what ECNative.allocateDirect would wrap
+        keep.append(hb)
+        return hb.array
+
     for t in range(T):
-        d = [np.random.default_rng(t * 8 + j).integers(0, 256, L, dtype=np.uint8) for j in range(k)]
-        p = [np.empty(L, np.uint8) for _ in range(m)]
+        d = []
+        for j in range(k):
+            a = host_array(L)
+            a[:] = np.random.default_rng(t * 8 + j).integers(0, 256, L, dtype=np.uint8)
+            d.append(a)
+        p = [host_array(L) for _ in range(m)]
         bufs.append((d, p))
+    if pinned and not all(_lib.host_pinned(x.ctypes.data, L) for d, p in bufs for x in d + p):
+        raise RuntimeError("--host-alloc pinned: elect_ec_host_alloc returned memory that is not page-locked")
     calls = max(4, args.steps // 2) * max(1, 4404020 // L // 8) * ndev
     fused = args.host_op == "encode_ex"
     content = [int(L / 1.05) - 64 * j for j in range(k)]  # SSTables just under codeLength/1.05
@@ -929,18 +948,20 @@ def config_hostpath(args, world, rank, dev):
     quota = host_cpu_info()["quota_cores"] or len(os.sched_getaffinity(0))
     return {"metric": f"GiB/s host-memory RS(6,4) {op_name} through the C ABI (JNI calling convention)",
             "value": round(data_gib / dt, 2), "unit": "GiB/s", "n_gpus": world,
-            "devices": ndev, "callers": T, "host_path_stats": stats,
+            "devices": ndev, "callers": T, "host_path_stats": stats, "host_alloc": args.host_alloc,
             # CPU time the whole process spent (every caller, helper and dispatcher thread) per GiB
             # of data coded: what the offload costs the node's cores
             "cpu_core_ms_per_GiB": round(core_ms, 2),
             # the rate this path could reach if the process's CPU quota were its only limit
             "cpu_bound_ceiling_GiB/s": round(quota * 1e3 / core_ms, 1) if core_ms > 0 else None,
             "cpu_quota_cores": quota,
-            "host_wait": os.environ.get("ELECT_EC_HOST_WAIT", "block"),
+            "host_wait": os.environ.get("ELECT_EC_HOST_WAIT", "callback"),
             "steps": done, "warmup": 1, "ms_per_step": round(dt / done * 1e3, 3), "higher_is_better": True,
             "scaling": "none", "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
             "config": {"workload": f"{T} threads x {done} synchronous elect_ec_{args.host_op} calls, one stripe "
-                                   f"of {k} x {L} B each, pageable host buffers, over {ndev} device(s)",
+                                   f"of {k} x {L} B each, "
+                                   f"{'elect_ec_host_alloc (page-locked)' if pinned else 'pageable'} host buffers, "
+                                   f"over {ndev} device(s)",
                        "parallelism": ("cross-thread batching (shared pinned arena, one launch per batch)"
                                        if args.batch else "per-thread pinned staging + 2 streams") +
                                       (f", callers spread over devices 0..{ndev - 1} (elect_ec_set_host_devices)"
@@ -951,12 +972,14 @@ HOSTPATH_CALLERS = 64  # ELECT's concurrent_ec (conf/elect.yaml:598)
 HOSTPATH_CHILD_TIMEOUT_S = 420
 
 
-def hostpath_child_cmd(ndev: int) -> list:
+def hostpath_child_cmd(ndev: int, alloc: str = "pageable") -> list:
     """The child process hostpath_all_devices starts: the JNI calling convention,
-    64 callers, ELECT's codeLength, batching on, callers over devices 0..ndev-1."""
+    64 callers, ELECT's codeLength, batching on, callers over devices 0..ndev-1;
+    alloc: the callers' buffers (pageable: ELECT as it is; pinned: ELECT with its
+    coding buffers from elect_ec_host_alloc)."""
     return [sys.executable, os.path.abspath(__file__), "--config", "hostpath", "--threads", str(HOSTPATH_CALLERS),
             "--host-chunk", "4404020", "--batch", "1", "--host-devices", str(ndev), "--steps", "8",
-            "--host-seconds", "2"]
+            "--host-seconds", "2", "--host-alloc", alloc]
 
 
 def child_env() -> dict:
@@ -983,26 +1006,35 @@ def hostpath_all_devices(args, world, rank, child=None):
     barrier(world)
     if rank == 0:
         ndev = world if child is not None else min(world, torch.cuda.device_count())
-        cmd = child if child is not None else hostpath_child_cmd(ndev)
-        try:  # (well inside the gloo group's 10-minute timeout the other ranks wait under)
-            r = subprocess.run(cmd, capture_output=True, text=True, env=child_env(), timeout=HOSTPATH_CHILD_TIMEOUT_S)
-        except subprocess.TimeoutExpired as e:
-            r = subprocess.CompletedProcess(cmd, -9, (e.stdout or b"").decode(errors="replace") if isinstance(
-                e.stdout, bytes) else (e.stdout or ""), f"timed out after {HOSTPATH_CHILD_TIMEOUT_S} s")
-        line = next((x for x in reversed(r.stdout.splitlines()) if x.startswith("{")), None)
-        if r.returncode != 0 or line is None:
-            res = {"verified": False, "devices": ndev, "error": f"rc={r.returncode}: {(r.stderr or r.stdout)[-400:]}"}
-        elif child is not None:
-            res = {"verified": True, "devices": ndev, "child": json.loads(line)}
-        else:
-            o = json.loads(line)
-            res = {"value": o["value"], "unit": o["unit"], "devices": o["devices"], "callers": o["callers"],
-                   "cpu_core_ms_per_GiB": o.get("cpu_core_ms_per_GiB"),
-                   "cpu_bound_ceiling_GiB/s": o.get("cpu_bound_ceiling_GiB/s"),
-                   "cpu_quota_cores": o.get("cpu_quota_cores"), "host_wait": o.get("host_wait"),
-                   "host_path_stats": o.get("host_path_stats"),
-                   "calls_per_caller": o["steps"], "verified": bool(o["verified"]),
-                   "workload": o["config"]["workload"], "parallelism": o["config"]["parallelism"]}
+        runs = [("pageable", child)] if child is not None else [("pageable", None), ("pinned", None)]
+        for alloc, cmd_override in runs:
+            cmd = cmd_override if cmd_override is not None else hostpath_child_cmd(ndev, alloc)
+            try:  # (well inside the gloo group's 10-minute timeout the other ranks wait under)
+                r = subprocess.run(cmd, capture_output=True, text=True, env=child_env(),
+                                   timeout=HOSTPATH_CHILD_TIMEOUT_S)
+            except subprocess.TimeoutExpired as e:
+                r = subprocess.CompletedProcess(cmd, -9, (e.stdout or b"").decode(errors="replace") if isinstance(
+                    e.stdout, bytes) else (e.stdout or ""), f"timed out after {HOSTPATH_CHILD_TIMEOUT_S} s")
+            line = next((x for x in reversed(r.stdout.splitlines()) if x.startswith("{")), None)
+            if r.returncode != 0 or line is None:
+                rec = {"verified": False, "devices": ndev, "error": f"rc={r.returncode}: {(r.stderr or r.stdout)[-400:]}"}
+            elif child is not None:
+                rec = {"verified": True, "devices": ndev, "child": json.loads(line)}
+            else:
+                o = json.loads(line)
+                rec = {"value": o["value"], "unit": o["unit"], "devices": o["devices"], "callers": o["callers"],
+                       "host_alloc": o.get("host_alloc"),
+                       "cpu_core_ms_per_GiB": o.get("cpu_core_ms_per_GiB"),
+                       "cpu_bound_ceiling_GiB/s": o.get("cpu_bound_ceiling_GiB/s"),
+                       "cpu_quota_cores": o.get("cpu_quota_cores"), "host_wait": o.get("host_wait"),
+                       "host_path_stats": o.get("host_path_stats"),
+                       "calls_per_caller": o["steps"], "verified": bool(o["verified"]),
+                       "workload": o["config"]["workload"], "parallelism": o["config"]["parallelism"]}
+            if res is None:
+                res = rec
+            else:  # ELECT with its coding buffers from elect_ec_host_alloc
+                res[alloc] = rec
+                res["verified"] = res["verified"] and rec["verified"]
     barrier(world)
     return res
 
@@ -1584,6 +1616,8 @@ def main():
         if rank == 0:
             out["hostpath_all_devices"] = hp
             out["hostpath_all_devices_GiB/s"] = hp.get("value")
+            if isinstance(hp.get("pinned"), dict):
+                out["hostpath_all_devices_pinned_GiB/s"] = hp["pinned"].get("value")
             rec["verified"] = rec["verified"] and hp["verified"]
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args, k, m, L, B)

@@ -77,6 +77,9 @@ SIGNATURES = [
     ("elect_ec_set_host_devices", ctypes.c_int, [_ip, ctypes.c_int]),
     ("elect_ec_set_batching", ctypes.c_int, [ctypes.c_int, ctypes.c_uint, ctypes.c_size_t]),
     ("elect_ec_host_path_stats", ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
+    ("elect_ec_host_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(_cp)]),
+    ("elect_ec_host_free", ctypes.c_int, [_cp]),
+    ("elect_ec_host_pinned", ctypes.c_int, [_cp, ctypes.c_size_t]),
     ("elect_ec_coder_create", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_cp)]),
     ("elect_ec_coder_destroy", None, [_cp]),
     ("elect_ec_coder_num_data_units", ctypes.c_int, [_cp]),
@@ -205,9 +208,48 @@ def set_batching(enable: bool, window_us: int = 0, arena_bytes: int = 256 << 20)
 
 def host_path_stats() -> dict:
     """The host-memory path's counters (elect_ec_host_path_stats)."""
-    out = (ctypes.c_uint64 * 4)()
-    lib.elect_ec_host_path_stats(out, 4)
-    return {"zero_copy": out[0], "zero_copy_fallback": out[1], "batched": out[2], "per_thread": out[3]}
+    out = (ctypes.c_uint64 * 5)()
+    lib.elect_ec_host_path_stats(out, 5)
+    return {"zero_copy": out[0], "zero_copy_fallback": out[1], "batched": out[2], "per_thread": out[3],
+            "direct": out[4]}
+
+
+def host_alloc(nbytes: int) -> int:
+    """Address of an elect_ec_host_alloc buffer of nbytes (page-locked when a device allows)."""
+    p = ctypes.c_void_p()
+    check(lib.elect_ec_host_alloc(nbytes, ctypes.byref(p)), "host_alloc")
+    return p.value
+
+
+def host_free(addr: int) -> None:
+    check(lib.elect_ec_host_free(addr), "host_free")
+
+
+def host_pinned(addr: int, nbytes: int) -> bool:
+    return bool(lib.elect_ec_host_pinned(addr, nbytes))
+
+
+class HostBuffer:
+    """An elect_ec_host_alloc buffer as a numpy uint8 array (what a JVM would wrap in a
+    direct ByteBuffer); freed on close() or garbage collection."""
+
+    def __init__(self, nbytes: int):
+        import numpy as np
+        self.addr = host_alloc(nbytes)
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_ubyte * nbytes).from_address(self.addr))
+
+    def close(self) -> None:
+        if self.addr:
+            self.array = None
+            host_free(self.addr)
+            self.addr = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def ptr_array(addrs) -> ctypes.Array:

@@ -300,6 +300,12 @@ int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes)
 
 int elect_ec_host_path_stats(uint64_t* out, int n) { return elect::host::host_path_stats(out, n); }
 
+int elect_ec_host_alloc(size_t bytes, void** out) { return elect::host::host_alloc(bytes, out); }
+
+int elect_ec_host_free(void* ptr) { return elect::host::host_free(ptr); }
+
+int elect_ec_host_pinned(const void* ptr, size_t bytes) { return elect::host::host_pinned(ptr, bytes); }
+
 int elect_ec_coder_create(int num_data_units, int num_parity_units, elect_ec_coder** out)
 {
     if (!out) return ELECT_EC_EINVAL;

@@ -14,7 +14,9 @@
 #include <cstring>
 #include <functional>
 #include <memory>
+#include <map>
 #include <mutex>
+#include <shared_mutex>
 #include <new>
 #include <string>
 #include <thread>
@@ -26,17 +28,19 @@ namespace {
 
 using kern::ApplyParams;
 
-// How host threads wait for the device (ELECT_EC_HOST_WAIT, read once).  HIP's
-// default waits poll: a thread in hipStreamSynchronize / hipEventSynchronize,
-// and the runtime thread behind a hipLaunchHostFunc callback, each keep a core
-// busy for as long as the device works.  On ELECT's storage
-// node those cores are the coding pool's.
-//   block (default): events created with hipEventBlockingSync; every wait is a
-//     blocking event wait (the thread sleeps until the interrupt); the batcher's
-//     completions come from a completion thread waiting on such events.
-//   spin: the same structure with polling events (A/B only).
-//   callback: round 3's waits: hipStreamSynchronize and host-function callbacks
-//     (A/B only).
+// How host threads wait for the device (ELECT_EC_HOST_WAIT, read once).
+//   callback (default): the batcher's completions come from a host-function
+//     callback (hipLaunchHostFunc) run by a HIP runtime thread; other waits are
+//     hipStreamSynchronize.
+//   block: events created with hipEventBlockingSync; every wait is a blocking
+//     event wait, and the batcher's completions come from a completion thread
+//     of its own waiting on such events.
+//   spin: the block structure with polling events.
+// Round 4 A/B (profiles/r04/hostwait_ab.txt, pageable buffers, ELECT's codeLength,
+// 2 interleaved rounds): at 64 callers callback 48.7-50.1 GiB/s at 204-227 core-ms
+// per GiB, block 42.8-43.5 at 234-255, spin 42.9-43.2 at 194-242: the CPU goes to
+// the staging copies, not to the waits, and the completion thread's hand-off
+// costs throughput.
 enum class WaitMode { kBlock, kSpin, kCallback };
 
 WaitMode wait_mode()
@@ -44,8 +48,8 @@ WaitMode wait_mode()
     static const WaitMode m = [] {
         const char* e = std::getenv("ELECT_EC_HOST_WAIT");
         if (e && std::strcmp(e, "spin") == 0) return WaitMode::kSpin;
-        if (e && std::strcmp(e, "callback") == 0) return WaitMode::kCallback;
-        return WaitMode::kBlock;
+        if (e && std::strcmp(e, "block") == 0) return WaitMode::kBlock;
+        return WaitMode::kCallback;
     }();
     return m;
 }
@@ -97,6 +101,129 @@ void stream_copy(uint8_t* dst, const uint8_t* src, size_t n)
         n -= body;
     }
     std::memcpy(dst, src, n);
+}
+
+// ---------------------------------------------------------------------------
+// Page-locked buffers for the callers' own units (elect_ec_host_alloc).  ELECT
+// allocates a direct ByteBuffer per unit and stripe and copies the SSTable into
+// it (ECMessageVerbHandler.java:298-314); when those buffers come from here,
+// the batcher moves a call's units by DMA straight between them and the device
+// (Batcher, direct batches): no staging copies, which are most of the CPU the
+// pageable path costs (1.5 bytes copied per data byte).
+// Pooled by size class (64 KiB steps): ELECT frees its buffers after every
+// stripe, and page-locking a 4.4 MB buffer costs far more than reusing one.
+// When page-locked memory cannot be had (no device, a locked-memory limit) the
+// allocation is ordinary memory, and calls on it take the staged path.
+// ---------------------------------------------------------------------------
+class PinnedPool {
+public:
+    static PinnedPool& get()
+    {
+        static PinnedPool* pool = new PinnedPool();  // never destroyed: buffers may outlive static teardown
+        return *pool;
+    }
+
+    void* alloc(size_t bytes)
+    {
+        const size_t cls = std::max<size_t>(kClass, (bytes + kClass - 1) / kClass * kClass);
+        {
+            std::unique_lock<std::shared_mutex> lock(mu_);
+            auto it = free_.find(cls);
+            if (it != free_.end() && !it->second.empty()) {
+                void* p = it->second.back();
+                it->second.pop_back();
+                free_bytes_ -= cls;
+                live_[reinterpret_cast<uintptr_t>(p)] = Block{cls, true};
+                return p;
+            }
+        }
+        void* p = nullptr;
+        bool pinned = hipHostMalloc(&p, cls, hipHostMallocPortable) == hipSuccess && p;
+        if (!pinned) {
+            (void)hipGetLastError();
+            p = std::aligned_alloc(4096, cls);
+            if (!p) return nullptr;
+        }
+        std::unique_lock<std::shared_mutex> lock(mu_);
+        live_[reinterpret_cast<uintptr_t>(p)] = Block{cls, pinned};
+        return p;
+    }
+
+    bool free(void* p)
+    {
+        Block b;
+        {
+            std::unique_lock<std::shared_mutex> lock(mu_);
+            auto it = live_.find(reinterpret_cast<uintptr_t>(p));
+            if (it == live_.end()) return false;
+            b = it->second;
+            live_.erase(it);
+            if (b.pinned && free_bytes_ + b.size <= cap()) {
+                free_[b.size].push_back(p);
+                free_bytes_ += b.size;
+                return true;
+            }
+        }
+        if (b.pinned)
+            (void)hipHostFree(p);
+        else
+            std::free(p);
+        return true;
+    }
+
+    // [p, p + n) lies inside one live page-locked block.
+    bool pinned(const void* p, size_t n) const
+    {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        std::shared_lock<std::shared_mutex> lock(mu_);
+        if (live_.empty()) return false;
+        auto it = live_.upper_bound(a);
+        if (it == live_.begin()) return false;
+        --it;
+        return it->second.pinned && a + n <= it->first + it->second.size;
+    }
+
+    bool any() const
+    {
+        std::shared_lock<std::shared_mutex> lock(mu_);
+        return !live_.empty();
+    }
+
+private:
+    static constexpr size_t kClass = size_t{1} << 16;
+    struct Block {
+        size_t size = 0;
+        bool pinned = false;
+    };
+
+    // free page-locked bytes kept for reuse (ELECT_EC_HOST_POOL_MB, default 4096)
+    static size_t cap()
+    {
+        static const size_t c = [] {
+            const char* e = std::getenv("ELECT_EC_HOST_POOL_MB");
+            return (e ? static_cast<size_t>(std::max(0, std::atoi(e))) : size_t{4096}) << 20;
+        }();
+        return c;
+    }
+
+    mutable std::shared_mutex mu_;
+    std::map<uintptr_t, Block> live_;
+    std::map<size_t, std::vector<void*>> free_;
+    size_t free_bytes_ = 0;
+};
+
+// Every byte the call reads and writes lies in page-locked pool buffers.
+bool direct_op(const HostOp& op, size_t len)
+{
+    PinnedPool& pool = PinnedPool::get();
+    if (!pool.any()) return false;
+    for (int j = 0; j < op.cols; ++j) {
+        const size_t n = op.lens ? op.lens[j] : len;
+        if (n && !pool.pinned(op.in[j], n)) return false;
+    }
+    for (int r = 0; r < op.rows; ++r)
+        if (!pool.pinned(op.out[r], len)) return false;
+    return true;
 }
 
 // Copy fan-out for lone callers.  One thread's staging copies (~20 GB/s) bound a
@@ -512,6 +639,8 @@ public:
     // Per-slot content lengths (padded ops) and parity hashes (hashed ops) of a
     // batch: entries per arena, which caps such a batch's stripes.
     static constexpr size_t kMetaEntries = size_t{1} << 16;
+    // Slots of a direct batch (each slot's unit pointers are kept in the slab).
+    static constexpr size_t kMaxDirectSlots = 1024;
     // A caller fans its copies out (CopyPool) while at most this many callers are
     // in flight (ELECT_EC_COPY_FANOUT_CALLERS, default 2).
     static int lone_callers()
@@ -525,7 +654,10 @@ public:
 
     explicit Batcher(int dev) : dev_(dev) {}
 
-    int submit(const HostOp& op, size_t len)
+    // direct: every unit of the call lies in page-locked pool memory (direct_op);
+    // its units then move by DMA between the caller's buffers and the device,
+    // with no staging copies, in batches of direct calls only.
+    int submit(const HostOp& op, size_t len, bool direct)
     {
         struct InFlight {  // callers inside submit(), for the copy fan-out policy
             std::atomic<int>& n;
@@ -533,7 +665,8 @@ public:
             ~InFlight() { n.fetch_sub(1); }
         } in_flight(callers_);
         // untiled: one unit per column at a 256-byte pitch; tiled: T tiles of 64 KiB
-        const size_t tile = batch_config().tile.load();
+        // (direct batches are untiled: one DMA per unit)
+        const size_t tile = direct ? 0 : batch_config().tile.load();
         // (tiled launches ride on the padded vector kernels: a wider product, the
         // update of an m >= 9 code, stays untiled rather than fail its whole batch)
         const bool tileable = op.cols <= kern::kMaxPadCols;
@@ -570,13 +703,13 @@ public:
         Slab* slab = nullptr;
         for (;;) {
             for (Slab& s : active())
-                if (s.state == Slab::kOpen && s.matches(op, len) && s.reserved < s.capacity) slab = &s;
+                if (s.state == Slab::kOpen && s.matches(op, len, direct) && s.reserved < s.capacity) slab = &s;
             if (!slab) {
                 for (Slab& s : active())  // a different shape or a full arena closes the open batch
                     if (s.state == Slab::kOpen) s.full = true;
                 for (Slab& s : active())
                     if (s.state == Slab::kFree) {
-                        s.open(op, len, pitch, tiles, arena_, ++opened_);
+                        s.open(op, len, pitch, tiles, arena_, ++opened_, direct);
                         slab = &s;
                         break;
                     }
@@ -597,10 +730,19 @@ public:
         for (int j = 0; j < op.cols; ++j) {
             const size_t n = op.lens ? op.lens[j] : len;  // padded: only the content bytes
             if (op.lens) slab->pin_lens[static_cast<size_t>(slot) * op.cols + j] = static_cast<uint32_t>(n);
+            if (direct) {  // the dispatcher DMAs it from the caller's buffer
+                slab->dsrc[static_cast<size_t>(slot) * kern::kMaxCols + j] = n ? op.in[j] : nullptr;
+                slab->dsrc_n[static_cast<size_t>(slot) * kern::kMaxCols + j] = n;
+                continue;
+            }
             for (size_t o = 0; o < n; o += pitch)  // untiled: pitch >= len, one copy
                 add_copy(jobs, in_base + (o / pitch * op.cols + j) * pitch, op.in[j] + o, std::min(pitch, n - o));
         }
-        run_copies(jobs, callers_.load() <= lone_callers());  // fenced before the dispatcher's H2D reads them
+        if (direct) {
+            for (int r = 0; r < op.rows; ++r) slab->ddst[static_cast<size_t>(slot) * kern::kMaxRows + r] = op.out[r];
+        } else {
+            run_copies(jobs, callers_.load() <= lone_callers());  // fenced before the dispatcher's H2D reads them
+        }
 
         lock.lock();
         if (++slab->filled == slab->reserved) cv_worker_.notify_one();
@@ -608,7 +750,7 @@ public:
         const int status = slab->status;
         lock.unlock();
 
-        if (status == ELECT_EC_OK) {
+        if (status == ELECT_EC_OK && !direct) {  // (direct: the D2H wrote the caller's buffers)
             const size_t out_stride = tiles * op.rows * pitch;
             const uint8_t* const out_base = slab->pin_out + slot * out_stride;
             jobs.clear();
@@ -619,9 +761,9 @@ public:
                              tiles > 1 ? std::min(pitch, len - o) : len);
                 }
             run_copies(jobs, callers_.load() <= lone_callers());
-            if (op.hashes)
-                std::memcpy(op.hashes, slab->pin_hash + static_cast<size_t>(slot) * op.rows, op.rows * sizeof(int32_t));
         }
+        if (status == ELECT_EC_OK && op.hashes)
+            std::memcpy(op.hashes, slab->pin_hash + static_cast<size_t>(slot) * op.rows, op.rows * sizeof(int32_t));
         lock.lock();
         if (--slab->readers == 0) {
             slab->state = Slab::kFree;
@@ -634,7 +776,7 @@ private:
     struct Shape {  // what a batch computes, copied out of its slab under mu_
         int cols = 0, rows = 0;
         size_t len = 0, pitch = 0, tiles = 1;
-        bool padded = false, hashed = false;
+        bool padded = false, hashed = false, direct = false;
         uint8_t coef[kern::kMaxRows * kern::kMaxCols] = {};
     };
 
@@ -646,7 +788,7 @@ private:
         uint8_t coef[kern::kMaxRows * kern::kMaxCols] = {};
         int capacity = 0, reserved = 0, filled = 0, readers = 0, status = ELECT_EC_OK;
         bool full = false;
-        bool padded = false, hashed = false;
+        bool padded = false, hashed = false, direct = false;
         uint64_t seq = 0;
         std::chrono::steady_clock::time_point opened;
         uint8_t *pin_in = nullptr, *pin_out = nullptr, *d_in = nullptr, *d_out = nullptr;
@@ -654,6 +796,10 @@ private:
         int32_t *pin_hash = nullptr, *d_hash = nullptr;    // [slot][rows]
         uint32_t* d_scratch = nullptr;                       // hash partials of the batch's launch
         size_t scratch_words = 0;
+        // direct batches: each slot's unit pointers and input byte counts, [slot][kMaxCols / kMaxRows]
+        std::unique_ptr<const uint8_t*[]> dsrc;
+        std::unique_ptr<size_t[]> dsrc_n;
+        std::unique_ptr<uint8_t*[]> ddst;
         std::condition_variable done;  // this batch's callers wait here for kDone
         hipStream_t stream = nullptr;
         hipEvent_t h2d_done = nullptr;
@@ -669,17 +815,18 @@ private:
             sh.tiles = tiles;
             sh.padded = padded;
             sh.hashed = hashed;
+            sh.direct = direct;
             std::memcpy(sh.coef, coef, sizeof(coef));
             return sh;
         }
 
-        bool matches(const HostOp& op, size_t n) const
+        bool matches(const HostOp& op, size_t n, bool d) const
         {
             return op.cols == cols && op.rows == rows && n == len && (op.lens != nullptr) == padded &&
-                   (op.hashes != nullptr) == hashed && std::memcmp(op.coef, coef, sizeof(coef)) == 0;
+                   (op.hashes != nullptr) == hashed && d == direct && std::memcmp(op.coef, coef, sizeof(coef)) == 0;
         }
 
-        void open(const HostOp& op, size_t n, size_t p, size_t t, size_t arena, uint64_t order)
+        void open(const HostOp& op, size_t n, size_t p, size_t t, size_t arena, uint64_t order, bool d)
         {
             cols = op.cols;
             rows = op.rows;
@@ -689,9 +836,11 @@ private:
             std::memcpy(coef, op.coef, sizeof(coef));
             padded = op.lens != nullptr;
             hashed = op.hashes != nullptr;
+            direct = d;
             size_t cap = arena / (static_cast<size_t>(std::max(cols, rows)) * pitch * tiles);
             if (padded) cap = std::min(cap, kMetaEntries / cols);
             if (hashed) cap = std::min(cap, kMetaEntries / rows);
+            if (direct) cap = std::min(cap, kMaxDirectSlots);
             capacity = static_cast<int>(cap);
             reserved = filled = readers = 0;
             status = ELECT_EC_OK;
@@ -724,6 +873,10 @@ private:
             s.scratch_words = kern::hash_scratch_need(arena / 16);  // a batch has at most arena/16 segments
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_scratch), s.scratch_words * sizeof(uint32_t));
             if (e != hipSuccess) return map_hip(e);
+            s.dsrc.reset(new (std::nothrow) const uint8_t*[kMaxDirectSlots * kern::kMaxCols]);
+            s.dsrc_n.reset(new (std::nothrow) size_t[kMaxDirectSlots * kern::kMaxCols]);
+            s.ddst.reset(new (std::nothrow) uint8_t*[kMaxDirectSlots * kern::kMaxRows]);
+            if (!s.dsrc || !s.dsrc_n || !s.ddst) return ELECT_EC_ENOMEM;
         }
         return ELECT_EC_OK;
     }
@@ -805,7 +958,18 @@ private:
     {
         const size_t in_stride = sh.tiles * sh.cols * sh.pitch;  // per slot
         const size_t out_stride = sh.tiles * sh.rows * sh.pitch;
-        hipError_t e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
+        hipError_t e = hipSuccess;
+        if (sh.direct) {  // every unit straight from its caller's page-locked buffer
+            for (int q = 0; q < n && e == hipSuccess; ++q)
+                for (int j = 0; j < sh.cols && e == hipSuccess; ++j) {
+                    const size_t i = static_cast<size_t>(q) * kern::kMaxCols + j;
+                    if (s.dsrc_n[i])
+                        e = hipMemcpyAsync(s.d_in + q * in_stride + j * sh.pitch, s.dsrc[i], s.dsrc_n[i],
+                                           hipMemcpyHostToDevice, s.stream);
+                }
+        } else {
+            e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
+        }
         if (e == hipSuccess && sh.padded)
             e = hipMemcpyAsync(s.d_lens, s.pin_lens, static_cast<size_t>(n) * sh.cols * sizeof(uint32_t),
                                hipMemcpyHostToDevice, s.stream);
@@ -839,7 +1003,14 @@ private:
             }
             e = kern::launch_apply(p, s.stream);
         }
-        if (e == hipSuccess) e = hipMemcpyAsync(s.pin_out, s.d_out, n * out_stride, hipMemcpyDeviceToHost, s.stream);
+        if (e == hipSuccess && sh.direct) {
+            for (int q = 0; q < n && e == hipSuccess; ++q)
+                for (int r = 0; r < sh.rows && e == hipSuccess; ++r)
+                    e = hipMemcpyAsync(s.ddst[static_cast<size_t>(q) * kern::kMaxRows + r], s.d_out + q * out_stride + r * sh.pitch,
+                                       sh.len, hipMemcpyDeviceToHost, s.stream);
+        } else if (e == hipSuccess) {
+            e = hipMemcpyAsync(s.pin_out, s.d_out, n * out_stride, hipMemcpyDeviceToHost, s.stream);
+        }
         if (e == hipSuccess && sh.hashed)
             e = hipMemcpyAsync(s.pin_hash, s.d_hash, static_cast<size_t>(n) * sh.rows * sizeof(int32_t),
                                hipMemcpyDeviceToHost, s.stream);
@@ -1100,8 +1271,10 @@ bool lone_caller(int dev)
     if (prev != me && prev != 0) g_other_caller_ns[dev].store(now);  // 0: no thread has called before
     return now - g_other_caller_ns[dev].load() > kAloneNs;
 }
-// elect_ec_host_path_stats: zero-copy calls, zero-copy fallbacks, batched, per-thread engine.
-std::atomic<uint64_t> g_stats[4];
+// elect_ec_host_path_stats: zero-copy calls, zero-copy fallbacks, batched (staged), per-thread
+// engine, batched direct (page-locked caller buffers, no staging copies).
+constexpr int kStats = 5;
+std::atomic<uint64_t> g_stats[kStats];
 
 }  // namespace
 
@@ -1136,7 +1309,10 @@ int run_host(const HostOp& op, size_t len)
     } in_flight(g_in_flight[dev]);
     try {  // nothing may unwind into the JVM: allocation failures become status codes
         rc = Batcher::kFallback;
-        if (ZeroCopy::eligible(op, len, in_flight.now, lone_caller(dev))) {
+        // units in page-locked pool buffers (elect_ec_host_alloc) move by DMA with no
+        // staging copy (batched); any other lone caller's may be page-locked for the call
+        const bool direct = direct_op(op, len);
+        if (!direct && ZeroCopy::eligible(op, len, in_flight.now, lone_caller(dev))) {
             rc = ZeroCopy::run(op, len);
             g_stats[rc == ZeroCopy::kFallback ? 1 : 0].fetch_add(1);
             if (rc == ZeroCopy::kFallback) rc = Batcher::kFallback;
@@ -1144,8 +1320,8 @@ int run_host(const HostOp& op, size_t len)
         }
         if (batch_config().enabled.load() == 1) {
             Batcher* b = batcher(dev);
-            rc = b ? b->submit(op, len) : ELECT_EC_ENOMEM;
-            if (rc != Batcher::kFallback) g_stats[2].fetch_add(1);
+            rc = b ? b->submit(op, len, direct) : ELECT_EC_ENOMEM;
+            if (rc != Batcher::kFallback) g_stats[direct ? 4 : 2].fetch_add(1);
         }
         if (rc == Batcher::kFallback) {
             if (!t_engines[dev]) t_engines[dev].reset(new (std::nothrow) HostEngine(dev));
@@ -1186,9 +1362,37 @@ int set_host_devices(const int* devices, int n)
 int host_path_stats(uint64_t* out, int n)
 {
     if (n < 0 || (n > 0 && !out)) return ELECT_EC_EINVAL;
-    const int w = n < 4 ? n : 4;
+    const int w = n < kStats ? n : kStats;
     for (int i = 0; i < w; ++i) out[i] = g_stats[i].load();
     return w;
+}
+
+int host_alloc(size_t bytes, void** out)
+{
+    if (!out) return ELECT_EC_EINVAL;
+    *out = nullptr;
+    if (bytes == 0) return ELECT_EC_EINVAL;
+    try {
+        *out = PinnedPool::get().alloc(bytes);
+    } catch (...) {
+        *out = nullptr;
+    }
+    return *out ? ELECT_EC_OK : ELECT_EC_ENOMEM;
+}
+
+int host_free(void* ptr)
+{
+    if (!ptr) return ELECT_EC_OK;
+    try {
+        return PinnedPool::get().free(ptr) ? ELECT_EC_OK : ELECT_EC_EINVAL;
+    } catch (...) {
+        return ELECT_EC_ENOMEM;
+    }
+}
+
+int host_pinned(const void* ptr, size_t bytes)
+{
+    return PinnedPool::get().pinned(ptr, bytes) ? 1 : 0;
 }
 
 int set_batching(int enable, unsigned window_us, size_t arena_bytes)

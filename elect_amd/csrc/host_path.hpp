@@ -53,6 +53,9 @@ int run_host(const HostOp& op, size_t len);
 int set_host_devices(const int* devices, int n);
 int set_batching(int enable, unsigned window_us, size_t arena_bytes);
 int host_path_stats(uint64_t* out, int n);  // elect_ec_host_path_stats
+int host_alloc(size_t bytes, void** out);    // elect_ec_host_alloc
+int host_free(void* ptr);                    // elect_ec_host_free
+int host_pinned(const void* ptr, size_t bytes);  // elect_ec_host_pinned
 
 }  // namespace host
 }  // namespace elect

@@ -9,7 +9,8 @@
  * INTEGRATION.md for the build line.  No Java code changes: ELECT keeps calling
  * System.loadLibrary("ec") (JEC/NativeRSEncoder.java:37).  Three optional
  * methods (encodeExImpl, encodeUpdateExImpl, decodeExImpl) expose the fused
- * coding-node steps to a Java that declares them.
+ * coding-node steps to a Java that declares them, and two more
+ * (allocateDirectImpl, freeDirectImpl) page-locked coding buffers.
  *
  * Differences from the reference glue, all on error paths:
  *  - every THROW returns (EC/NativeRSDecoder.c:50-52 and EC/jni_common.c:70-73,
@@ -354,6 +355,46 @@ Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_destroyImpl(JNIEnv* env
         elect_ec_coder_destroy(c);
         set_coder(env, thiz, NULL);
     }
+}
+
+/* Optional: page-locked direct buffers for ELECT's coding buffers
+ * ("Page-locked coding buffers").  Declared in NativeRSEncoder.java as
+ *   static native ByteBuffer allocateDirectImpl(int capacity);
+ *   static native void freeDirectImpl(ByteBuffer buffer);
+ * ELECT's ByteBuffer.allocateDirect(codeLength) calls for its data and parity units
+ * (ECMessageVerbHandler.java:298, 314) become allocateDirectImpl; a call whose units
+ * all live in such buffers is moved by DMA with no staging copies (elect_ec_host_alloc). */
+JNIEXPORT jobject JNICALL
+Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_allocateDirectImpl(JNIEnv* env, jclass cls, jint capacity)
+{
+    void* p = NULL;
+    jobject buf;
+    (void)cls;
+    if (capacity < 0) {
+        throw_java(env, "java/lang/IllegalArgumentException", "allocateDirect: negative capacity");
+        return NULL;
+    }
+    if (raise_status(env, elect_ec_host_alloc(capacity > 0 ? (size_t)capacity : 1, &p), "allocateDirect"))
+        return NULL;
+    buf = (*env)->NewDirectByteBuffer(env, p, (jlong)capacity);
+    if (buf == NULL)  /* the JVM has an OutOfMemoryError pending */
+        elect_ec_host_free(p);
+    return buf;
+}
+
+JNIEXPORT void JNICALL
+Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_freeDirectImpl(JNIEnv* env, jclass cls, jobject buffer)
+{
+    void* p;
+    (void)cls;
+    if (buffer == NULL)
+        return;
+    p = (*env)->GetDirectBufferAddress(env, buffer);
+    if (p == NULL) {
+        throw_java(env, "java/lang/IllegalArgumentException", "freeDirect: not a direct buffer");
+        return;
+    }
+    raise_status(env, elect_ec_host_free(p), "freeDirect");
 }
 
 JNIEXPORT void JNICALL

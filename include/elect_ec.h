@@ -121,9 +121,29 @@ int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes);
  * out[0] zero-copy calls (a lone caller's buffers page-locked and coded in
  * place over PCIe; ELECT_EC_ZEROCOPY=0 off, 1 default, 2 every eligible call),
  * out[1] zero-copy attempts that fell back (registration refused), out[2]
- * calls coded through the cross-thread batcher, out[3] calls coded by the
- * per-thread staging engine.  Writes min(n, 4) entries; returns the count. */
+ * calls coded through the cross-thread batcher with staging copies, out[3]
+ * calls coded by the per-thread staging engine, out[4] calls coded through the
+ * batcher by DMA straight from and to elect_ec_host_alloc buffers.  Writes
+ * min(n, 5) entries; returns the count. */
 int elect_ec_host_path_stats(uint64_t* out, int n);
+
+/* Page-locked host memory for the units of host-memory calls.  ELECT allocates
+ * a direct ByteBuffer per unit and stripe (ECMessageVerbHandler.java:298-314,
+ * ECParityUpdateVerbHandler.java, ECRecovery.java) and copies its SSTable
+ * into it; allocated here instead (NewDirectByteBuffer over this memory, see
+ * INTEGRATION.md), a call whose every unit lies in such buffers is moved by DMA
+ * straight between them and the device, with no staging copies: the bulk of
+ * the CPU the host path costs on pageable buffers.  Pooled (64 KiB size
+ * classes, ELECT_EC_HOST_POOL_MB of free buffers kept, default 4096): freeing
+ * and allocating one size per stripe reuses the same page-locked memory.
+ * When page-locked memory is unavailable the buffer is ordinary memory and
+ * calls on it take the staged path; *out is NULL only when no memory at all
+ * could be had (ELECT_EC_ENOMEM).  Usable from any thread; free with
+ * elect_ec_host_free (EINVAL for a pointer not from elect_ec_host_alloc). */
+int elect_ec_host_alloc(size_t bytes, void** out);
+int elect_ec_host_free(void* ptr);
+/* 1 when [ptr, ptr + bytes) lies in one page-locked elect_ec_host_alloc buffer. */
+int elect_ec_host_pinned(const void* ptr, size_t bytes);
 
 /* ---- coder lifecycle ----
  * Replaces initEncoder / initDecoder (EC/erasure_coder.c:49-72) as called by

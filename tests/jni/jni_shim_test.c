@@ -236,6 +236,16 @@ static void* m_GetDirectBufferAddress(JNIEnv* env, jobject o)
     return o->kind == K_DIRECT ? o->addr : NULL;
 }
 
+static jobject m_NewDirectByteBuffer(JNIEnv* env, void* addr, jlong capacity)
+{
+    (void)env;
+    no_pending("NewDirectByteBuffer");
+    jobject o = new_obj(K_DIRECT, "java/nio/DirectByteBuffer");
+    o->addr = addr;
+    o->n = (int)capacity;
+    return o;
+}
+
 static void m_DeleteLocalRef(JNIEnv* env, jobject o)
 {
     (void)env;  /* exception-safe per the JNI spec */
@@ -262,6 +272,7 @@ static const struct JNINativeInterface_ kEnvTable = {
     .GetIntArrayRegion = m_GetIntArrayRegion,
     .SetIntArrayRegion = m_SetIntArrayRegion,
     .ExceptionCheck = m_ExceptionCheck,
+    .NewDirectByteBuffer = m_NewDirectByteBuffer,
     .GetDirectBufferAddress = m_GetDirectBufferAddress,
 };
 static JNIEnv kEnv = &kEnvTable;
@@ -291,7 +302,10 @@ static struct {
     encode_ex_fn encode_ex;
     update_ex_fn update_ex;
     decode_ex_fn decode_ex;
+    jobject (*alloc_direct)(JNIEnv*, jclass, jint);
+    void (*free_direct)(JNIEnv*, jclass, jobject);
     int (*device_count)(int*);
+    int (*host_pinned)(const void*, size_t);
 } jni;
 
 static void* sym(void* h, const char* name)
@@ -322,7 +336,10 @@ static void load(const char* lib)
     jni.encode_ex = (encode_ex_fn)sym(h, PFX "NativeRSEncoder_encodeExImpl");
     jni.update_ex = (update_ex_fn)sym(h, PFX "NativeRSEncoder_encodeUpdateExImpl");
     jni.decode_ex = (decode_ex_fn)sym(h, PFX "NativeRSDecoder_decodeExImpl");
+    jni.alloc_direct = (jobject(*)(JNIEnv*, jclass, jint))sym(h, PFX "NativeRSEncoder_allocateDirectImpl");
+    jni.free_direct = (void (*)(JNIEnv*, jclass, jobject))sym(h, PFX "NativeRSEncoder_freeDirectImpl");
     jni.device_count = (int (*)(int*))sym(h, "elect_ec_device_count");
+    jni.host_pinned = (int (*)(const void*, size_t))sym(h, "elect_ec_host_pinned");
 }
 
 /* ---- Java-side object builders ------------------------------------------- */
@@ -545,6 +562,27 @@ static int cpu_checks(void)
     jni.decode_ex(env, dec, in4, off4, NULL, 16, int_array(4, di4), int_array(1, er1), out1, poff1);
     EXPECT(threw("java/io/IOException", "NativeRSRawDecoder closed"));
 
+    /* page-locked coding buffers: argument errors; without a device the buffer is ordinary memory */
+    jclass enc_cls = new_obj(K_CLASS, ENC_CLS);
+    EXPECT(jni.alloc_direct(env, enc_cls, -1) == NULL);
+    EXPECT(threw("java/lang/IllegalArgumentException", "negative capacity"));
+    jobject bb = jni.alloc_direct(env, enc_cls, 4099);
+    EXPECT(clean() && bb != NULL && bb->kind == K_DIRECT && bb->n == 4099);
+    if (bb) {
+        memset(bb->addr, 0x5A, 4099);  /* the whole capacity is writable */
+        jni.free_direct(env, enc_cls, bb);
+        EXPECT(clean());
+        jni.free_direct(env, enc_cls, bb);  /* twice: not a live buffer any more */
+        EXPECT(threw("java/lang/IllegalArgumentException", "freeDirect"));
+    }
+    unsigned char foreign[64];
+    jni.free_direct(env, enc_cls, direct_bb(foreign));
+    EXPECT(threw("java/lang/IllegalArgumentException", "freeDirect"));
+    jni.free_direct(env, enc_cls, new_obj(K_HEAP, "java/nio/HeapByteBuffer"));
+    EXPECT(threw("java/lang/IllegalArgumentException", "not a direct buffer"));
+    jni.free_direct(env, enc_cls, NULL);
+    EXPECT(clean());
+
     EXPECT(vm.violations == 0);
     EXPECT(vm.live_int_elems == 0);
     EXPECT(vm.local_refs == 0);
@@ -731,6 +769,32 @@ static int gpu_fused_flows(void)
     EXPECT(!memcmp(at(&rb, 0), at(&newd, 0), ulens[1]));
     EXPECT(at(&rb, 0)[ulens[1]] == 0x33);  /* nothing past the requested prefix is written */
     jni.dec_destroy(env, dec);
+
+    /* ELECT's encode with its units in allocateDirectImpl buffers (page-locked: the
+     * engine moves them by DMA, no staging copy) equals the encode of ordinary ones */
+    jclass enc_cls = new_obj(K_CLASS, ENC_CLS);
+    jobject pin_in[K], pin_out[M];
+    jint zero_pos[K] = {0, 0, 0, 0};
+    for (int i = 0; i < K; ++i) {
+        pin_in[i] = jni.alloc_direct(env, enc_cls, L);
+        EXPECT(clean() && pin_in[i] != NULL && jni.host_pinned(pin_in[i]->addr, (size_t)L));
+        memcpy(pin_in[i]->addr, at(&filled, i), L);
+    }
+    for (int r = 0; r < M; ++r) {
+        pin_out[r] = jni.alloc_direct(env, enc_cls, L);
+        EXPECT(clean() && pin_out[r] != NULL);
+        memset(pin_out[r]->addr, 0xCC, L);
+    }
+    jni.encode(env, enc, obj_array(K, pin_in), int_array(K, zero_pos), L, obj_array(M, pin_out),
+               int_array(M, zero_pos));
+    EXPECT(clean());
+    jni.encode(env, enc, obj_array(K, filled.bb), int_array(K, filled.pos), L, obj_array(M, ref.bb),
+               int_array(M, ref.pos));
+    EXPECT(clean());
+    for (int r = 0; r < M; ++r) EXPECT(!memcmp(pin_out[r]->addr, at(&ref, r), L));
+    for (int i = 0; i < K; ++i) jni.free_direct(env, enc_cls, pin_in[i]);
+    for (int r = 0; r < M; ++r) jni.free_direct(env, enc_cls, pin_out[r]);
+    EXPECT(clean());
     jni.enc_destroy(env, enc);
     EXPECT(vm.violations == 0);
     EXPECT(vm.live_int_elems == 0);

@@ -6,7 +6,8 @@
  * types and the JNIEnv function table LAID OUT AS THE JNI SPECIFICATION DEFINES
  * IT ("JNI Functions: Interface Function Table"): 235 pointer slots in the
  * specification's order (slots 0-3 reserved, FindClass at 6, ...,
- * GetDirectBufferAddress at 230, up to IsVirtualThread at 234), with the slots
+ * NewDirectByteBuffer at 229, GetDirectBufferAddress at 230, up to IsVirtualThread
+ * at 234), with the slots
  * the shim calls named and typed as in the JDK header and every other slot
  * kept as padding.  The static asserts below pin each named slot's index, so a
  * library built against this header calls the same table entries a JDK-built
@@ -83,7 +84,7 @@ struct JNINativeInterface_ {
     void (*SetIntArrayRegion)(JNIEnv*, jintArray, jsize, jsize, const jint*); /* 211 */
     void* unused_212_227[16];
     jboolean (*ExceptionCheck)(JNIEnv*); /* 228 */
-    void* unused_229;
+    jobject (*NewDirectByteBuffer)(JNIEnv*, void*, jlong); /* 229 */
     void* (*GetDirectBufferAddress)(JNIEnv*, jobject); /* 230 */
     void* unused_231_234[4];
 };
@@ -108,6 +109,7 @@ JNI_SLOT(ReleaseIntArrayElements, 195);
 JNI_SLOT(GetIntArrayRegion, 203);
 JNI_SLOT(SetIntArrayRegion, 211);
 JNI_SLOT(ExceptionCheck, 228);
+JNI_SLOT(NewDirectByteBuffer, 229);
 JNI_SLOT(GetDirectBufferAddress, 230);
 _Static_assert(sizeof(struct JNINativeInterface_) == 235 * sizeof(void*), "JNI function table size (JDK 21)");
 _Static_assert(sizeof(jint) == 4 && sizeof(jlong) == 8 && sizeof(jboolean) == 1, "JNI primitive sizes");

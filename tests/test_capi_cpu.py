@@ -241,3 +241,30 @@ def test_device_api_rejects_mismatched_shapes():
     # a tiled view with a zero tile length: ValueError, not ZeroDivisionError
     with pytest.raises(ValueError, match="tile"):
         encode_batch_tiled(c, st[:, :4, :0], st[:, 4:, :0], 64)
+
+
+def test_host_alloc_pool_semantics():
+    """elect_ec_host_alloc / _free / _pinned: every allocation is usable memory
+    (page-locked when a device allows, ordinary memory otherwise, which the host
+    path then stages), frees are checked, and the pinned query covers exactly a
+    live page-locked buffer."""
+    from elect_amd import _lib
+    bufs = [_lib.HostBuffer(n) for n in (1, 4096, 65536 + 3, 4404020)]
+    for b in bufs:
+        b.array[:] = 0xA5  # writable over its whole length
+        assert int(b.array[-1]) == 0xA5
+        pinned = _lib.host_pinned(b.addr, b.nbytes)
+        assert pinned == (gpu_available() and _lib.device_count() > 0)
+        assert not _lib.host_pinned(b.addr, b.nbytes + (1 << 16) + 1)  # past the 64 KiB size class
+    addr = bufs[-1].addr
+    for b in bufs:
+        b.close()
+    assert not _lib.host_pinned(addr, 16)  # freed (kept in the pool, not live)
+    with pytest.raises(_lib.ECInvalidArgument):
+        _lib.host_free(addr)  # not live any more
+    x = np.zeros(64, np.uint8)
+    with pytest.raises(_lib.ECInvalidArgument):
+        _lib.host_free(x.ctypes.data)  # never allocated here
+    assert _lib.lib.elect_ec_host_free(None) == 0
+    p = ctypes.c_void_p()
+    assert _lib.lib.elect_ec_host_alloc(0, ctypes.byref(p)) == _lib.EINVAL and not p.value

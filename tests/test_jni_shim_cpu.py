@@ -13,10 +13,14 @@ import numpy as np
 
 from tests.jni_build import build
 
-OPTIONAL = {  # fused coding-node steps, bound only by a Java that declares them
+OPTIONAL = {  # bound only by a Java that declares them
+    # the fused coding-node steps
     "Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeExImpl",
     "Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_encodeUpdateExImpl",
     "Java_org_apache_cassandra_io_erasurecode_NativeRSDecoder_decodeExImpl",
+    # page-locked coding buffers (elect_ec_host_alloc)
+    "Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_allocateDirectImpl",
+    "Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_freeDirectImpl",
 }
 SEVEN = {
     "Java_org_apache_cassandra_io_erasurecode_NativeRSEncoder_initImpl",
@@ -29,7 +33,7 @@ SEVEN = {
 }
 
 
-def test_shim_exports_the_seven_native_methods_and_the_three_optional_ones():
+def test_shim_exports_the_seven_native_methods_and_the_optional_ones():
     lib, _ = build()
     out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
     exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
@@ -125,7 +129,7 @@ def test_mock_jni_table_is_the_specification_layout():
             "GetMethodID": 33, "CallBooleanMethod": 37, "GetFieldID": 94, "GetLongField": 101, "SetLongField": 110,
             "GetArrayLength": 171, "GetObjectArrayElement": 173, "GetIntArrayElements": 187,
             "ReleaseIntArrayElements": 195, "GetIntArrayRegion": 203, "SetIntArrayRegion": 211,
-            "ExceptionCheck": 228, "GetDirectBufferAddress": 230}
+            "ExceptionCheck": 228, "NewDirectByteBuffer": 229, "GetDirectBufferAddress": 230}
     for name, idx in want.items():
         assert f"JNI_SLOT({name}, {idx});" in text, name
     shim = open(os.path.join(ROOT, "elect_amd", "csrc", "jni", "libec_jni.c")).read()

@@ -246,6 +246,11 @@ for step in "$@"; do
             ELECT_EC_HOST_WAIT=$w run "hostwait_${w}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
                 --host-op ${HOST_OP:-encode} --host-seconds ${HOST_S:-2} || exit $?
         done; done; done ;;
+    hostdirect)  # page-locked caller buffers (elect_ec_host_alloc, direct batches) vs pageable, x waits (round 4)
+        for i in 1 2; do for al in ${ALLOCS:-pinned pageable}; do for w in ${WAIT_MODES:-callback block}; do for T in ${WAIT_T:-1 16 64}; do
+            ELECT_EC_HOST_WAIT=$w run "hostdirect_${al}_${w}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
+                --host-op ${HOST_OP:-encode} --host-seconds ${HOST_S:-2} --host-alloc $al || exit $?
+        done; done; done; done ;;
     padfill)  # padded encode vs content fill: where the time goes
         for f in 1.0 0.0 0.5 random; do
             run "bench_padded_fill_$f" 300 python bench.py --config padded --pad-fill $f || exit $?
