@@ -5,7 +5,8 @@
 // the reference is safe only with a coder per task (EC/NativeRSEncoder.c:25-29).
 // Here T threads share ONE coder and mix every host entry point (encode, encode_ex
 // padded/hashed, encode_update_ex, decode_ex with prefix lengths) at random
-// lengths, with cross-thread batching on, then off.  Each result is checked by an
+// lengths, with cross-thread batching on, then off, then on units in the engine's
+// page-locked pool (direct batches).  Each result is checked by an
 // independent route: decode(encode(x)) == x, update == re-encode, and the JDK
 // ByteBuffer.hashCode loop written out here.  Exit 0 = no mismatch (and, under
 // ASan/UBSan, no memory or UB error in the host code: batcher arenas, staging,
@@ -32,6 +33,56 @@ static int32_t java_hash(const uint8_t* p, size_t n)
     return static_cast<int32_t>(h);
 }
 
+// A byte buffer in ordinary memory or in the engine's page-locked pool
+// (elect_ec_host_alloc): calls whose every unit is pooled run as direct batches,
+// moved by DMA with no staging copies.
+struct Buf {
+    uint8_t* p = nullptr;
+    size_t n = 0;
+    bool pool = false;
+    Buf() = default;
+    Buf(size_t len, bool pooled, uint8_t fill = 0) { make(len, pooled, fill); }
+    Buf(const Buf& o)
+    {
+        make(o.n, o.pool, 0);
+        std::memcpy(p, o.p, n);
+    }
+    Buf& operator=(const Buf& o)
+    {
+        if (this != &o) {
+            drop();
+            make(o.n, o.pool, 0);
+            std::memcpy(p, o.p, n);
+        }
+        return *this;
+    }
+    ~Buf() { drop(); }
+    void make(size_t len, bool pooled, uint8_t fill)
+    {
+        n = len;
+        pool = pooled;
+        void* q = nullptr;
+        if (pooled ? elect_ec_host_alloc(len ? len : 1, &q) != 0 : !(q = std::malloc(len ? len : 1))) std::abort();
+        p = static_cast<uint8_t*>(q);
+        std::memset(p, fill, n);
+    }
+    void drop()
+    {
+        if (!p) return;
+        if (pool)
+            (void)elect_ec_host_free(p);
+        else
+            std::free(p);
+        p = nullptr;
+    }
+    uint8_t* data() { return p; }
+    const uint8_t* data() const { return p; }
+    uint8_t* begin() { return p; }
+    uint8_t* end() { return p + n; }
+    uint8_t& operator[](size_t i) { return p[i]; }
+    bool operator==(const Buf& o) const { return n == o.n && std::memcmp(p, o.p, n) == 0; }
+};
+
 #define CHECK(cond, ...)                                \
     do {                                                \
         if (!(cond)) {                                  \
@@ -41,14 +92,14 @@ static int32_t java_hash(const uint8_t* p, size_t n)
         }                                               \
     } while (0)
 
-static void worker(const elect_ec_coder* c, int k, int m, int tid, int iters, size_t big = 0)
+static void worker(const elect_ec_coder* c, int k, int m, int tid, int iters, size_t big = 0, bool pooled = false)
 {
     std::mt19937_64 rng(1000 + tid);
     auto rnd = [&](size_t lo, size_t hi) { return lo + rng() % (hi - lo + 1); };
     for (int it = 0; it < iters; ++it) {
         // big: units of big/3..big bytes, so that a lone caller's copies fan out (CopyPool)
         const size_t L = big ? rnd(big / 3, big) : rng() % 4 == 0 ? rnd(1, 64) : rnd(1000, 300000);
-        std::vector<std::vector<uint8_t>> d(k, std::vector<uint8_t>(L)), p(m, std::vector<uint8_t>(L));
+        std::vector<Buf> d(k, Buf(L, pooled)), p(m, Buf(L, pooled));
         std::vector<size_t> lens(k);
         for (int j = 0; j < k; ++j) {
             for (auto& b : d[j]) b = static_cast<uint8_t>(rng());
@@ -81,7 +132,7 @@ static void worker(const elect_ec_coder* c, int k, int m, int tid, int iters, si
             sl.push_back(u < k && padded ? lens[u] : L);
         }
         const size_t pre = rnd(0, L);
-        std::vector<uint8_t> rebuilt(L + 1, 0xA5);
+        Buf rebuilt(L + 1, pooled, 0xA5);
         uint8_t* ro[1] = {rebuilt.data()};
         st = elect_ec_decode_ex(c, sv.data(), padded ? sl.data() : nullptr, di.data(), &e, 1, ro, pre,
                                 ELECT_EC_DECODE_COMPAT);
@@ -91,7 +142,7 @@ static void worker(const elect_ec_coder* c, int k, int m, int tid, int iters, si
 
         // parity update of unit t in place, then compare with a fresh encode
         const int t = static_cast<int>(rng() % k);
-        std::vector<uint8_t> nw(L);
+        Buf nw(L, pooled);
         for (auto& b : nw) b = static_cast<uint8_t>(rng());
         const size_t ul[2] = {padded ? lens[t] : L, padded ? rnd(0, L) : L};
         std::vector<const uint8_t*> ui = {d[t].data(), nw.data()};
@@ -101,7 +152,7 @@ static void worker(const elect_ec_coder* c, int k, int m, int tid, int iters, si
         CHECK(st == 0, "t%d it%d update_ex status %d\n", tid, it, st);
         std::memset(nw.data() + ul[1], 0, L - ul[1]);
         d[t] = nw;
-        std::vector<std::vector<uint8_t>> q(m, std::vector<uint8_t>(L));
+        std::vector<Buf> q(m, Buf(L, pooled));
         std::vector<uint8_t*> qo(m);
         for (int r = 0; r < m; ++r) qo[r] = q[r].data();
         for (int j = 0; j < k; ++j) in[j] = d[j].data();
@@ -193,7 +244,7 @@ int main(int argc, char** argv)
         if (batching > first) continue;
         elect_ec_set_batching(batching, 0, size_t{8} << 20);  // small arenas: batches close often
         std::vector<std::thread> th;
-        for (int t = 0; t < threads; ++t) th.emplace_back(worker, c, 4, 2, t + 100 * batching, iters, size_t{0});
+        for (int t = 0; t < threads; ++t) th.emplace_back(worker, c, 4, 2, t + 100 * batching, iters, size_t{0}, false);
         for (auto& x : th) x.join();
         std::printf("batching=%d: %d threads x %d iterations, failures so far %d\n", batching, threads, iters,
                     g_fail.load());
@@ -202,10 +253,21 @@ int main(int argc, char** argv)
         elect_ec_set_batching(1, 0, size_t{8} << 20);
         for (int n : {1, 2}) {
             std::vector<std::thread> th;
-            for (int t = 0; t < n; ++t) th.emplace_back(worker, c, 4, 2, t + 200 + 10 * n, iters, size_t{1900000});
+            for (int t = 0; t < n; ++t) th.emplace_back(worker, c, 4, 2, t + 200 + 10 * n, iters, size_t{1900000}, false);
             for (auto& x : th) x.join();
         }
         std::printf("lone callers: 1 and 2 threads x %d iterations, failures so far %d\n", iters, g_fail.load());
+    }
+    {  // every unit in page-locked pool buffers: direct batches (no staging copies), pool reuse across threads
+        elect_ec_set_batching(1, 0, size_t{8} << 20);
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t) th.emplace_back(worker, c, 4, 2, t + 300, iters, size_t{0}, true);
+        for (auto& x : th) x.join();
+        uint64_t st[5] = {};
+        elect_ec_host_path_stats(st, 5);
+        std::printf("pool buffers: %d threads x %d iterations, direct calls %llu, failures so far %d\n", threads, iters,
+                    static_cast<unsigned long long>(st[4]), g_fail.load());
+        CHECK(st[4] > 0, "no call took the direct path\n");
     }
     {
         std::vector<std::thread> th;
