@@ -955,7 +955,6 @@ def config_hostpath(args, world, rank, dev):
             # the rate this path could reach if the process's CPU quota were its only limit
             "cpu_bound_ceiling_GiB/s": round(quota * 1e3 / core_ms, 1) if core_ms > 0 else None,
             "cpu_quota_cores": quota,
-            "host_wait": os.environ.get("ELECT_EC_HOST_WAIT", "callback"),
             "steps": done, "warmup": 1, "ms_per_step": round(dt / done * 1e3, 3), "higher_is_better": True,
             "scaling": "none", "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
             "config": {"workload": f"{T} threads x {done} synchronous elect_ec_{args.host_op} calls, one stripe "
@@ -1026,7 +1025,7 @@ def hostpath_all_devices(args, world, rank, child=None):
                        "host_alloc": o.get("host_alloc"),
                        "cpu_core_ms_per_GiB": o.get("cpu_core_ms_per_GiB"),
                        "cpu_bound_ceiling_GiB/s": o.get("cpu_bound_ceiling_GiB/s"),
-                       "cpu_quota_cores": o.get("cpu_quota_cores"), "host_wait": o.get("host_wait"),
+                       "cpu_quota_cores": o.get("cpu_quota_cores"),
                        "host_path_stats": o.get("host_path_stats"),
                        "calls_per_caller": o["steps"], "verified": bool(o["verified"]),
                        "workload": o["config"]["workload"], "parallelism": o["config"]["parallelism"]}

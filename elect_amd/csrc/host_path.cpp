@@ -9,7 +9,6 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
-#include <deque>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -28,47 +27,16 @@ namespace {
 
 using kern::ApplyParams;
 
-// How host threads wait for the device (ELECT_EC_HOST_WAIT, read once).
-//   callback (default): the batcher's completions come from a host-function
-//     callback (hipLaunchHostFunc) run by a HIP runtime thread; other waits are
-//     hipStreamSynchronize.
-//   block: events created with hipEventBlockingSync; every wait is a blocking
-//     event wait, and the batcher's completions come from a completion thread
-//     of its own waiting on such events.
-//   spin: the block structure with polling events.
-// Round 4 A/B (profiles/r04/hostwait_ab.txt, pageable buffers, ELECT's codeLength,
-// 2 interleaved rounds): at 64 callers callback 48.7-50.1 GiB/s at 204-227 core-ms
-// per GiB, block 42.8-43.5 at 234-255, spin 42.9-43.2 at 194-242: the CPU goes to
-// the staging copies, not to the waits, and the completion thread's hand-off
-// costs throughput.
-enum class WaitMode { kBlock, kSpin, kCallback };
-
-WaitMode wait_mode()
-{
-    static const WaitMode m = [] {
-        const char* e = std::getenv("ELECT_EC_HOST_WAIT");
-        if (e && std::strcmp(e, "spin") == 0) return WaitMode::kSpin;
-        if (e && std::strcmp(e, "block") == 0) return WaitMode::kBlock;
-        return WaitMode::kCallback;
-    }();
-    return m;
-}
-
-hipError_t make_wait_event(hipEvent_t* ev)
-{
-    const unsigned flags = hipEventDisableTiming | (wait_mode() == WaitMode::kBlock ? hipEventBlockingSync : 0u);
-    return hipEventCreateWithFlags(ev, flags);
-}
-
-// Waits until everything enqueued on `s` so far is done: a blocking wait on
-// `ev` (recorded here), or hipStreamSynchronize in callback mode.
-hipError_t wait_stream(hipStream_t s, hipEvent_t ev)
-{
-    if (wait_mode() == WaitMode::kCallback || !ev) return hipStreamSynchronize(s);
-    hipError_t e = hipEventRecord(ev, s);
-    if (e == hipSuccess) e = hipEventSynchronize(ev);
-    return e;
-}
+// Host threads wait for the device with hipStreamSynchronize, and the batcher's
+// completions come from a host-function callback (hipLaunchHostFunc).  Round 4
+// measured the alternative the round-3 review proposed: events created with
+// hipEventBlockingSync and a completion thread of the batcher's own sleeping on
+// them (profiles/r04/hostwait_ab.txt, host_direct_ab.txt; 2 interleaved rounds,
+// ELECT's codeLength).  It saved no CPU and lost throughput everywhere: 64
+// callers on pageable buffers 48.6-49.3 -> 42.7-43.0 GiB/s, on page-locked
+// buffers 45.3 -> 39.5 GiB/s at 48 -> 58 core-ms per GiB.  On pageable buffers
+// the CPU goes to the staging copies; page-locked coding buffers remove those
+// (PinnedPool below, 4x less CPU per GiB).
 
 // Host copies into and out of the pinned staging memory, with non-temporal
 // (streaming) stores: the data is not read again by this CPU (the DMA engine
@@ -212,6 +180,16 @@ private:
     size_t free_bytes_ = 0;
 };
 
+// Streams a direct batch spreads its per-unit DMAs over (ELECT_EC_DIRECT_STREAMS, 1 or 2).
+int direct_streams()
+{
+    static const int n = [] {
+        const char* e = std::getenv("ELECT_EC_DIRECT_STREAMS");
+        return e && std::atoi(e) == 1 ? 1 : 2;
+    }();
+    return n;
+}
+
 // Every byte the call reads and writes lies in page-locked pool buffers.
 bool direct_op(const HostOp& op, size_t len)
 {
@@ -354,7 +332,6 @@ public:
     {
         for (int s = 0; s < kSlots; ++s) {
             if (stream_[s]) (void)hipStreamDestroy(stream_[s]);
-            if (ev_[s]) (void)hipEventDestroy(ev_[s]);
             if (pin_in_[s]) (void)hipHostFree(pin_in_[s]);
             if (pin_out_[s]) (void)hipHostFree(pin_out_[s]);
             if (d_in_[s]) (void)hipFree(d_in_[s]);
@@ -374,7 +351,7 @@ public:
         if (op.hashes) {  // every chunk's kernel adds into d_hash_; start from 31^len
             hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_hash_),
                                              static_cast<int>(kern::pow31(len)), op.rows, stream_[0]);
-            if (e == hipSuccess) e = wait_stream(stream_[0], ev_[0]);
+            if (e == hipSuccess) e = hipStreamSynchronize(stream_[0]);
             if (e != hipSuccess) return map_hip(e);
         }
         size_t pending[kSlots] = {};
@@ -382,7 +359,7 @@ public:
         for (size_t c = 0; c < nchunks + kSlots; ++c) {
             const int s = static_cast<int>(c % kSlots);
             if (busy[s]) {  // retire the chunk that used this slot
-                const hipError_t e = wait_stream(stream_[s], ev_[s]);
+                const hipError_t e = hipStreamSynchronize(stream_[s]);
                 if (e != hipSuccess) return map_hip(e);
                 const size_t o = pending[s] * step;
                 const size_t n = std::min(step, len - o);
@@ -414,8 +391,8 @@ public:
             if (e == hipSuccess)
                 e = hipMemcpyAsync(pin_out_[s], d_out_[s], op.rows * pitch, hipMemcpyDeviceToHost, stream_[s]);
             if (e != hipSuccess) {
-                (void)wait_stream(stream_[0], ev_[0]);
-                (void)wait_stream(stream_[1], ev_[1]);
+                (void)hipStreamSynchronize(stream_[0]);
+                (void)hipStreamSynchronize(stream_[1]);
                 return map_hip(e);
             }
             pending[s] = c;
@@ -457,8 +434,7 @@ private:
     {
         if (!stream_[0]) {
             for (int s = 0; s < kSlots; ++s) {
-                hipError_t e = hipStreamCreateWithFlags(&stream_[s], hipStreamNonBlocking);
-                if (e == hipSuccess) e = make_wait_event(&ev_[s]);
+                const hipError_t e = hipStreamCreateWithFlags(&stream_[s], hipStreamNonBlocking);
                 if (e != hipSuccess) return map_hip(e);
             }
             hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_hash_), kern::kMaxRows * sizeof(int32_t));
@@ -501,7 +477,6 @@ private:
 
     int dev_;
     hipStream_t stream_[kSlots] = {};
-    hipEvent_t ev_[kSlots] = {};  // blocking waits on the slots' streams (wait_stream)
     uint8_t* pin_in_[kSlots] = {};
     uint8_t* pin_out_[kSlots] = {};
     uint8_t* d_in_[kSlots] = {};
@@ -687,11 +662,8 @@ public:
                 return kFallback;
             }
             try {
-                // the completion thread first: a dispatcher without it would strand its batches
-                if (wait_mode() != WaitMode::kCallback) std::thread(&Batcher::completer, this).detach();
-                std::thread(&Batcher::worker, this).detach();  // both live as long as the process
+                std::thread(&Batcher::worker, this).detach();  // lives as long as the process
             } catch (...) {  // no dispatcher: the per-thread engine serves every call
-                // (a completion thread that did start only ever waits for batches that never come)
                 release();
                 init_failed_ = true;
                 return kFallback;
@@ -803,7 +775,9 @@ private:
         std::condition_variable done;  // this batch's callers wait here for kDone
         hipStream_t stream = nullptr;
         hipEvent_t h2d_done = nullptr;
-        hipEvent_t done_ev = nullptr;  // recorded behind the batch's D2H (the completion thread waits on it)
+        // direct batches: a second stream for half of the per-unit DMAs, and its fork/join events
+        hipStream_t stream2 = nullptr;
+        hipEvent_t fork = nullptr, join = nullptr;
 
         Shape shape() const
         {
@@ -858,8 +832,10 @@ private:
         for (Slab& s : active()) {
             s.owner = this;
             hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
-            if (e == hipSuccess) e = make_wait_event(&s.h2d_done);
-            if (e == hipSuccess) e = make_wait_event(&s.done_ev);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream2, hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&s.fork, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&s.join, hipEventDisableTiming);
             // device first: an arena too large for the device fails there, before any host pinning
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_in), arena);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_out), arena);
@@ -887,7 +863,9 @@ private:
         for (Slab& s : active()) {
             if (s.stream) (void)hipStreamDestroy(s.stream);
             if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
-            if (s.done_ev) (void)hipEventDestroy(s.done_ev);
+            if (s.stream2) (void)hipStreamDestroy(s.stream2);
+            for (hipEvent_t ev : {s.fork, s.join})
+                if (ev) (void)hipEventDestroy(ev);
             for (uint8_t* h : {s.pin_in, s.pin_out})
                 if (h) (void)hipHostFree(h);
             for (void* h : {static_cast<void*>(s.pin_lens), static_cast<void*>(s.pin_hash)})
@@ -897,7 +875,8 @@ private:
                 if (d) (void)hipFree(d);
             s.stream = nullptr;
             s.h2d_done = nullptr;
-            s.done_ev = nullptr;
+            s.stream2 = nullptr;
+            s.fork = s.join = nullptr;
             s.pin_in = s.pin_out = s.d_in = s.d_out = nullptr;
             s.pin_lens = s.d_lens = nullptr;
             s.pin_hash = s.d_hash = nullptr;
@@ -940,14 +919,9 @@ private:
             const int n = s->reserved;
             lock.unlock();
             const hipError_t e = issue(*s, shape, n);
-            if (e != hipSuccess) (void)hipStreamSynchronize(s->stream);  // no completion was queued
+            if (e != hipSuccess) (void)hipStreamSynchronize(s->stream);  // no callback was queued
             lock.lock();
-            if (e != hipSuccess) {
-                finish(s, map_hip(e));
-            } else if (wait_mode() != WaitMode::kCallback) {
-                completing_.push_back(s);
-                cv_complete_.notify_one();
-            }
+            if (e != hipSuccess) finish(s, map_hip(e));
             prev = s;
         }
     }
@@ -959,14 +933,30 @@ private:
         const size_t in_stride = sh.tiles * sh.cols * sh.pitch;  // per slot
         const size_t out_stride = sh.tiles * sh.rows * sh.pitch;
         hipError_t e = hipSuccess;
+        // direct batches spread their per-unit DMAs over two streams, slot by slot
+        // (forked from and joined back into the slab's stream)
+        const bool two = sh.direct && direct_streams() > 1;
+        auto lane = [&](int q) { return two && (q & 1) ? s.stream2 : s.stream; };
+        auto fork = [&]() {
+            hipError_t r = hipEventRecord(s.fork, s.stream);
+            if (r == hipSuccess) r = hipStreamWaitEvent(s.stream2, s.fork, 0);
+            return r;
+        };
+        auto join = [&]() {
+            hipError_t r = hipEventRecord(s.join, s.stream2);
+            if (r == hipSuccess) r = hipStreamWaitEvent(s.stream, s.join, 0);
+            return r;
+        };
         if (sh.direct) {  // every unit straight from its caller's page-locked buffer
+            if (two) e = fork();
             for (int q = 0; q < n && e == hipSuccess; ++q)
                 for (int j = 0; j < sh.cols && e == hipSuccess; ++j) {
                     const size_t i = static_cast<size_t>(q) * kern::kMaxCols + j;
                     if (s.dsrc_n[i])
                         e = hipMemcpyAsync(s.d_in + q * in_stride + j * sh.pitch, s.dsrc[i], s.dsrc_n[i],
-                                           hipMemcpyHostToDevice, s.stream);
+                                           hipMemcpyHostToDevice, lane(q));
                 }
+            if (two && e == hipSuccess) e = join();
         } else {
             e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
         }
@@ -1004,40 +994,20 @@ private:
             e = kern::launch_apply(p, s.stream);
         }
         if (e == hipSuccess && sh.direct) {
+            if (two) e = fork();
             for (int q = 0; q < n && e == hipSuccess; ++q)
                 for (int r = 0; r < sh.rows && e == hipSuccess; ++r)
                     e = hipMemcpyAsync(s.ddst[static_cast<size_t>(q) * kern::kMaxRows + r], s.d_out + q * out_stride + r * sh.pitch,
-                                       sh.len, hipMemcpyDeviceToHost, s.stream);
+                                       sh.len, hipMemcpyDeviceToHost, lane(q));
+            if (two && e == hipSuccess) e = join();
         } else if (e == hipSuccess) {
             e = hipMemcpyAsync(s.pin_out, s.d_out, n * out_stride, hipMemcpyDeviceToHost, s.stream);
         }
         if (e == hipSuccess && sh.hashed)
             e = hipMemcpyAsync(s.pin_hash, s.d_hash, static_cast<size_t>(n) * sh.rows * sizeof(int32_t),
                                hipMemcpyDeviceToHost, s.stream);
-        if (e == hipSuccess)
-            e = wait_mode() == WaitMode::kCallback ? hipLaunchHostFunc(s.stream, &Batcher::on_done, &s)
-                                                   : hipEventRecord(s.done_ev, s.stream);
+        if (e == hipSuccess) e = hipLaunchHostFunc(s.stream, &Batcher::on_done, &s);
         return e;
-    }
-
-    // Completion thread (block and spin modes): waits for the issued batches in
-    // issue order, each on the event behind its D2H, and hands every batch back
-    // to its callers.  With blocking events it sleeps while the device works; a
-    // host-function callback (callback mode) is run by a HIP runtime thread
-    // that polls instead.
-    void completer()
-    {
-        (void)hipSetDevice(dev_);
-        std::unique_lock<std::mutex> lock(mu_);
-        for (;;) {
-            cv_complete_.wait(lock, [&] { return !completing_.empty(); });
-            Slab* s = completing_.front();
-            completing_.pop_front();
-            lock.unlock();
-            const hipError_t e = hipEventSynchronize(s->done_ev);
-            lock.lock();
-            finish(s, map_hip(e));
-        }
     }
 
     static void on_done(void* arg)  // HIP host-function callback: no HIP calls in here
@@ -1067,8 +1037,6 @@ private:
     std::mutex mu_;
     std::condition_variable cv_worker_;  // the dispatcher
     std::condition_variable cv_slot_;    // callers waiting for an arena to reserve in
-    std::condition_variable cv_complete_;  // the completion thread
-    std::deque<Slab*> completing_;         // issued batches, in issue order (under mu_)
     bool started_ = false;
     bool init_failed_ = false;  // the arenas could not be allocated: every call runs directly
     size_t arena_ = 0;
@@ -1167,19 +1135,17 @@ struct ZeroCopy {
         return m;
     }
 
-    // This thread's stream and wait event per device, destroyed when the thread
-    // exits (ELECT's coding pools retire threads).
+    // This thread's stream per device, destroyed when the thread exits (ELECT's
+    // coding pools retire threads).
     struct ThreadStreams {
         hipStream_t stream[kMaxDevices] = {};
-        hipEvent_t done[kMaxDevices] = {};
         ~ThreadStreams()
         {
             for (int d = 0; d < kMaxDevices; ++d) {
-                if (!stream[d] && !done[d]) continue;
+                if (!stream[d]) continue;
                 int prev = 0;
                 const bool other = hipGetDevice(&prev) == hipSuccess && prev != d && hipSetDevice(d) == hipSuccess;
-                if (done[d]) (void)hipEventDestroy(done[d]);
-                if (stream[d]) (void)hipStreamDestroy(stream[d]);
+                (void)hipStreamDestroy(stream[d]);
                 if (other) (void)hipSetDevice(prev);
             }
         }
@@ -1190,16 +1156,10 @@ struct ZeroCopy {
         thread_local ThreadStreams ts;
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return kFallback;
-        if (!ts.stream[dev]) {
-            if (hipStreamCreateWithFlags(&ts.stream[dev], hipStreamNonBlocking) != hipSuccess) {
-                ts.stream[dev] = nullptr;
-                (void)hipGetLastError();
-                return kFallback;
-            }
-            if (make_wait_event(&ts.done[dev]) != hipSuccess) {
-                ts.done[dev] = nullptr;  // wait_stream then synchronizes the stream itself
-                (void)hipGetLastError();
-            }
+        if (!ts.stream[dev] && hipStreamCreateWithFlags(&ts.stream[dev], hipStreamNonBlocking) != hipSuccess) {
+            ts.stream[dev] = nullptr;
+            (void)hipGetLastError();
+            return kFallback;
         }
         hipStream_t stream = ts.stream[dev];
         const auto rs = ranges(op, len);
@@ -1236,7 +1196,7 @@ struct ZeroCopy {
                 hipError_t e = kern::launch_apply(p, stream);
                 // Whatever was enqueued finishes before the pages are unregistered,
                 // also when a later launch of the call failed.
-                const hipError_t w = wait_stream(stream, ts.done[dev]);
+                const hipError_t w = hipStreamSynchronize(stream);
                 if (e == hipSuccess) e = w;
                 // A shape the single launch does not take (hipErrorInvalidValue is
                 // returned before the kernels run: a wide padded update past 2^31

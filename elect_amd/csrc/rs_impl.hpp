@@ -859,6 +859,8 @@ struct LaunchPolicy {
     // the per-lane form uncapped (caps of 24 / 28 cost 5 / 3 points, profiles/r02_hash_ab/)
     int hashed_block = 64;
     int hashed_scalar_waves = 20;
+    int hashed_lane_waves = 0;
+    int hashed_scalar_base_min_cols = 1;  // hashed launches take the scalar-base form from this width up
     // Padded launches: gf_apply_x16<PAD> (uncapped) and gf_apply_lens (capped).
     int padded_write_block = 128;    // random fill 68.9 -> 71.8 %, full 82.3 -> 82.7 % (block_pad_ab.txt);
                                      // read-heavy ones keep the plain block (64 / 128: -3 / -4 points)
@@ -921,7 +923,7 @@ inline LaunchShape launch_shape(Family f, int cols, int rows, uint64_t len, bool
     case Family::kPlain:
         if (len > P.small_len && !wide) return {64, one_wave_cap};
         return {plain_block, multi_cap};
-    case Family::kPlainHashed: return {P.hashed_block, scalar_base ? P.hashed_scalar_waves : 0};
+    case Family::kPlainHashed: return {P.hashed_block, scalar_base ? P.hashed_scalar_waves : P.hashed_lane_waves};
     case Family::kPadded:
     case Family::kLens: {
         const int block = write_heavy ? std::min(P.padded_write_block, plain_block) : plain_block;
@@ -998,7 +1000,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     // scalar stripe bases: plain launches of whole-wave stripes (kPolicy.scalar_base_min_cols
     // columns and up; hashed ones of any width)
     const bool whole_waves = !PAD && a.segs % 64 == 0 && segs64 < (uint64_t{1} << 28);
-    const bool scalar_base = whole_waves && (p.hashes ? K <= kMaxHashCols : K >= kPolicy.scalar_base_min_cols);
+    const bool scalar_base = whole_waves && (p.hashes ? K <= kMaxHashCols && K >= kPolicy.hashed_scalar_base_min_cols
+                                                      : K >= kPolicy.scalar_base_min_cols);
     // stripes per launch keeping idx < 2^31, whole logical stripes (tiles) per launch
     const uint64_t per_launch = kMaxIndex / segs64 / tiles * tiles;
     for (uint64_t s0 = 0; s0 < p.stripes; s0 += per_launch) {

@@ -251,6 +251,11 @@ for step in "$@"; do
             ELECT_EC_HOST_WAIT=$w run "hostdirect_${al}_${w}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
                 --host-op ${HOST_OP:-encode} --host-seconds ${HOST_S:-2} --host-alloc $al || exit $?
         done; done; done; done ;;
+    directstreams)  # direct batches: per-unit DMAs on 1 or 2 streams (round 4)
+        for i in 1 2; do for ds in 2 1; do for T in ${WAIT_T:-64 16 1}; do
+            ELECT_EC_DIRECT_STREAMS=$ds run "directstreams_s${ds}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
+                --host-seconds ${HOST_S:-2} --host-alloc pinned || exit $?
+        done; done; done ;;
     padfill)  # padded encode vs content fill: where the time goes
         for f in 1.0 0.0 0.5 random; do
             run "bench_padded_fill_$f" 300 python bench.py --config padded --pad-fill $f || exit $?
