@@ -41,6 +41,9 @@ def units():
             out.append((src, os.path.splitext(src)[0], []))
     return out
 FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"]
+# Translation units with no device code, compiled as host C++ against the HIP runtime API.
+HOST_SOURCES = {"host_path.cpp"}
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include"]
 
 
 def digest_files(paths, extra: str = "") -> str:
@@ -55,7 +58,7 @@ def digest_files(paths, extra: str = "") -> str:
 
 def build_id() -> str:
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "elect_ec.h")]
-    return digest_files(deps, " ".join(FLAGS))
+    return digest_files(deps, " ".join(FLAGS + HOST_FLAGS + sorted(HOST_SOURCES)))
 
 
 def stamped_id() -> str | None:
@@ -88,7 +91,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
     def compile_one(unit):
         src, stem, extra = unit
         obj = os.path.join(BUILD, stem + ".o")
-        cmd = [hipcc, *common, *extra, "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
+        if src in HOST_SOURCES:  # no device code: host C++ (CPU builtins such as __builtin_cpu_supports)
+            cmd = [hipcc, *HOST_FLAGS, "-I", os.path.join(ROOT, "include"), f'-DELECT_EC_BUILD_ID="{bid}"',
+                   *extra, "-x", "c++", "-c", os.path.join(CSRC, src), "-o", obj]
+        else:
+            cmd = [hipcc, *common, *extra, "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         r = subprocess.run(cmd, capture_output=True, text=True)

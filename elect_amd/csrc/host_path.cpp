@@ -3,7 +3,7 @@
 // (EC/NativeRSEncoder.c:43-61 -> EC/erasure_coder.c:74-98).
 #include "host_path.hpp"
 
-#include <emmintrin.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -44,26 +44,58 @@ using kern::ApplyParams;
 // of the destination lines would only double the host-DRAM traffic this path
 // is bound by.  glibc's memcpy streams only above its non-temporal threshold,
 // which 64 KiB tile copies are far below.  Callers fence (_mm_sfence) before
-// the data is handed on.
+// the data is handed on.  The body moves 64-byte lines: AVX-512 (one 64-byte
+// streaming store fills a write-combining buffer) where the CPU has it,
+// else SSE2 (ELECT_EC_COPY_ISA=sse forces it, for A/B).
+__attribute__((target("avx512f"))) void stream_lines_avx512(uint8_t* dst, const uint8_t* src, size_t n)
+{
+    for (size_t i = 0; i < n; i += 128) {  // n % 128 == 0, dst 64-byte aligned
+        const __m512i a = _mm512_loadu_si512(src + i);
+        const __m512i b = _mm512_loadu_si512(src + i + 64);
+        _mm512_stream_si512(reinterpret_cast<__m512i*>(dst + i), a);
+        _mm512_stream_si512(reinterpret_cast<__m512i*>(dst + i + 64), b);
+    }
+}
+
+void stream_lines_sse(uint8_t* dst, const uint8_t* src, size_t n)
+{
+    for (size_t i = 0; i < n; i += 64) {  // n % 64 == 0, dst 16-byte aligned
+        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+    }
+}
+
+bool copy_avx512()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("ELECT_EC_COPY_ISA");
+        if (e && std::strcmp(e, "sse") == 0) return false;
+        __builtin_cpu_init();
+        return __builtin_cpu_supports("avx512f") != 0;
+    }();
+    return on;
+}
+
 void stream_copy(uint8_t* dst, const uint8_t* src, size_t n)
 {
     if (n >= 4096) {
-        const size_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
+        const size_t head = (64 - (reinterpret_cast<uintptr_t>(dst) & 63)) & 63;
         std::memcpy(dst, src, head);
         dst += head;
         src += head;
         n -= head;
-        const size_t body = n & ~size_t{63};
-        for (size_t i = 0; i < body; i += 64) {
-            const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
-            const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
-            const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
-            const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
-            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
-            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
-            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
-            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
-        }
+        const bool wide = copy_avx512();
+        const size_t body = n & ~static_cast<size_t>(wide ? 127 : 63);
+        if (wide)
+            stream_lines_avx512(dst, src, body);
+        else
+            stream_lines_sse(dst, src, body);
         dst += body;
         src += body;
         n -= body;
@@ -475,7 +507,7 @@ private:
         return ELECT_EC_OK;
     }
 
-    int dev_;
+    [[maybe_unused]] int dev_;
     hipStream_t stream_[kSlots] = {};
     uint8_t* pin_in_[kSlots] = {};
     uint8_t* pin_out_[kSlots] = {};

@@ -20,10 +20,14 @@ build)
     mkdir -p $OUT
     C="$H --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -I include $SAN"
     objs=""
-    for f in ec_capi.cpp host_path.cpp rs_kernels.hip; do
+    for f in ec_capi.cpp rs_kernels.hip; do
         $C -x hip -c elect_amd/csrc/$f -o $OUT/${f%.*}.o &
         objs="$objs $OUT/${f%.*}.o"
     done
+    # host_path.cpp has no device code: host C++ (elect_amd/build.py HOST_SOURCES)
+    $H -O1 -g -std=c++17 -fPIC -I include -I /opt/rocm/include -D__HIP_PLATFORM_AMD__ $SAN -x c++ \
+        -c elect_amd/csrc/host_path.cpp -o $OUT/host_path.o &
+    objs="$objs $OUT/host_path.o"
     for k in $(seq 1 16); do  # rs_inst.hip once per source-column count
         $C -DELECT_EC_INST_K=$k -x hip -c elect_amd/csrc/rs_inst.hip -o $OUT/rs_inst_k$k.o &
         objs="$objs $OUT/rs_inst_k$k.o"
