@@ -951,7 +951,10 @@ private:
             const int n = s->reserved;
             lock.unlock();
             const hipError_t e = issue(*s, shape, n);
-            if (e != hipSuccess) (void)hipStreamSynchronize(s->stream);  // no callback was queued
+            if (e != hipSuccess) {  // no callback was queued: drain both streams before the callers get their buffers back
+                (void)hipStreamSynchronize(s->stream);
+                (void)hipStreamSynchronize(s->stream2);
+            }
             lock.lock();
             if (e != hipSuccess) finish(s, map_hip(e));
             prev = s;
@@ -1108,7 +1111,9 @@ Batcher* batcher(int dev)
 // GiB/s against the batch's 44), so only a lone caller takes it.  ELECT_EC_ZEROCOPY: 0 off, 1 (default) lone callers with
 // units of at least kMinBytes, 2 every eligible call (tests).  Hashed calls keep
 // the staged path.  Any registration failure (memory already locked by another
-// call, a mapping the driver refuses) falls back to the staged path.
+// call, a mapping the driver refuses) falls back to the staged path.  Units in
+// the engine's page-locked pool (direct_op) need no registration: the kernel
+// reads and writes them where they are.
 // ---------------------------------------------------------------------------
 struct ZeroCopy {
     static constexpr size_t kMinBytes = size_t{1} << 20;  // mmap-backed buffers: no page shared with another caller
@@ -1183,7 +1188,9 @@ struct ZeroCopy {
         }
     };
 
-    static int run(const HostOp& op, size_t len)
+    // pinned: every unit already lies in the engine's page-locked pool (direct_op):
+    // nothing to register, the device reads and writes the pool buffers in place.
+    static int run(const HostOp& op, size_t len, bool pinned)
     {
         thread_local ThreadStreams ts;
         int dev = 0;
@@ -1194,7 +1201,7 @@ struct ZeroCopy {
             return kFallback;
         }
         hipStream_t stream = ts.stream[dev];
-        const auto rs = ranges(op, len);
+        const auto rs = pinned ? std::vector<std::pair<uintptr_t, uintptr_t>>{} : ranges(op, len);
         size_t locked = 0;
         for (; locked < rs.size(); ++locked)
             if (hipHostRegister(reinterpret_cast<void*>(rs[locked].first), rs[locked].second - rs[locked].first,
@@ -1304,8 +1311,8 @@ int run_host(const HostOp& op, size_t len)
         // units in page-locked pool buffers (elect_ec_host_alloc) move by DMA with no
         // staging copy (batched); any other lone caller's may be page-locked for the call
         const bool direct = direct_op(op, len);
-        if (!direct && ZeroCopy::eligible(op, len, in_flight.now, lone_caller(dev))) {
-            rc = ZeroCopy::run(op, len);
+        if (ZeroCopy::eligible(op, len, in_flight.now, lone_caller(dev))) {
+            rc = ZeroCopy::run(op, len, direct);
             g_stats[rc == ZeroCopy::kFallback ? 1 : 0].fetch_add(1);
             if (rc == ZeroCopy::kFallback) rc = Batcher::kFallback;
             else goto done;

@@ -70,7 +70,10 @@ def test_direct_entry_points_match_oracle(dev, oracle, L):
     wantd = oracle.decode(K, M, [_zf(x, n) for x, n in zip(ins, il)], [1, 2, 3, 4], [0])[1][0]
     assert np.array_equal(r, wantd)
     dl = _delta(st)
-    assert dl["direct"] == 4 and dl["zero_copy"] == 0 and dl["batched"] == 0, dl
+    # every call in place on the pool buffers: batched by DMA (direct), or, for a lone
+    # caller's unhashed calls of 1 MiB and up, read and written by the kernel over PCIe
+    assert dl["direct"] + dl["zero_copy"] == 4 and dl["direct"] >= 1, dl
+    assert dl["batched"] == 0 and dl["per_thread"] == 0 and dl["zero_copy_fallback"] == 0, dl
     for hb in keep:
         hb.close()
 
@@ -86,7 +89,8 @@ def test_direct_needs_every_unit_in_the_pool(dev, oracle):
     st = _lib.host_path_stats()
     RSCoder(K, M).encode_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L)
     assert all(np.array_equal(a, b) for a, b in zip(p, oracle.Encoder(K, M).encode(list(d))))
-    assert _delta(st)["direct"] == 0
+    dl = _delta(st)
+    assert dl["direct"] == 0 and dl["batched"] + dl["zero_copy"] + dl["per_thread"] == 1, dl
     for hb in keep:
         hb.close()
 
@@ -128,4 +132,4 @@ def test_direct_and_staged_callers_concurrently(dev, oracle):
         x.join()
     assert not errors, errors[:4]
     dl = _delta(st)
-    assert dl["direct"] == T // 2 * calls, dl
+    assert dl["direct"] + dl["zero_copy"] >= T // 2 * calls and dl["direct"] >= 1, dl

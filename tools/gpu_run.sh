@@ -256,6 +256,11 @@ for step in "$@"; do
             ELECT_EC_DIRECT_STREAMS=$ds run "directstreams_s${ds}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
                 --host-seconds ${HOST_S:-2} --host-alloc pinned || exit $?
         done; done; done ;;
+    pinzc)  # a lone caller on pool buffers: zero-copy in place (default) vs direct batches (round 4)
+        for i in 1 2; do for z in 1 0; do
+            ELECT_EC_ZEROCOPY=$z run "pinzc_z${z}_$i" 300 python bench.py --config hostpath --threads 1 \
+                --host-seconds ${HOST_S:-2} --host-alloc pinned || exit $?
+        done; done ;;
     copyisa)  # pageable staging copies: AVX-512 vs SSE2 streaming stores (round 4)
         for i in 1 2; do for isa in avx512 sse; do for T in ${WAIT_T:-64 16 1}; do
             ELECT_EC_COPY_ISA=$isa run "copyisa_${isa}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
