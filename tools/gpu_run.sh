@@ -256,6 +256,8 @@ for step in "$@"; do
             ELECT_EC_DIRECT_STREAMS=$ds run "directstreams_s${ds}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
                 --host-seconds ${HOST_S:-2} --host-alloc pinned || exit $?
         done; done; done ;;
+    ldsprobe)  # HBM streams loaded through LDS (global_load_lds_dwordx4) vs into VGPRs (round 4; build tools/tune/lds_probe first)
+        run ldsprobe 300 tools/tune/lds_probe || exit $? ;;
     pinzc)  # a lone caller on pool buffers: zero-copy in place (default) vs direct batches (round 4)
         for i in 1 2; do for z in 1 0; do
             ELECT_EC_ZEROCOPY=$z run "pinzc_z${z}_$i" 300 python bench.py --config hostpath --threads 1 \
