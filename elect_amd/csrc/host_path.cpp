@@ -3,7 +3,7 @@
 // (EC/NativeRSEncoder.c:43-61 -> EC/erasure_coder.c:74-98).
 #include "host_path.hpp"
 
-#include <immintrin.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -44,58 +44,28 @@ using kern::ApplyParams;
 // of the destination lines would only double the host-DRAM traffic this path
 // is bound by.  glibc's memcpy streams only above its non-temporal threshold,
 // which 64 KiB tile copies are far below.  Callers fence (_mm_sfence) before
-// the data is handed on.  The body moves 64-byte lines: AVX-512 (one 64-byte
-// streaming store fills a write-combining buffer) where the CPU has it,
-// else SSE2 (ELECT_EC_COPY_ISA=sse forces it, for A/B).
-__attribute__((target("avx512f"))) void stream_lines_avx512(uint8_t* dst, const uint8_t* src, size_t n)
-{
-    for (size_t i = 0; i < n; i += 128) {  // n % 128 == 0, dst 64-byte aligned
-        const __m512i a = _mm512_loadu_si512(src + i);
-        const __m512i b = _mm512_loadu_si512(src + i + 64);
-        _mm512_stream_si512(reinterpret_cast<__m512i*>(dst + i), a);
-        _mm512_stream_si512(reinterpret_cast<__m512i*>(dst + i + 64), b);
-    }
-}
-
-void stream_lines_sse(uint8_t* dst, const uint8_t* src, size_t n)
-{
-    for (size_t i = 0; i < n; i += 64) {  // n % 64 == 0, dst 16-byte aligned
-        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
-        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
-        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
-        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
-        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
-        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
-        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
-        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
-    }
-}
-
-bool copy_avx512()
-{
-    static const bool on = [] {
-        const char* e = std::getenv("ELECT_EC_COPY_ISA");
-        if (e && std::strcmp(e, "sse") == 0) return false;
-        __builtin_cpu_init();
-        return __builtin_cpu_supports("avx512f") != 0;
-    }();
-    return on;
-}
-
+// the data is handed on.  (AVX-512 64-byte streaming stores measured no better:
+// 64 callers the same, 16 callers 32.0-35.8 against 40.6-42.8 GiB/s,
+// profiles/r04/copy_isa_ab.txt.)
 void stream_copy(uint8_t* dst, const uint8_t* src, size_t n)
 {
     if (n >= 4096) {
-        const size_t head = (64 - (reinterpret_cast<uintptr_t>(dst) & 63)) & 63;
+        const size_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
         std::memcpy(dst, src, head);
         dst += head;
         src += head;
         n -= head;
-        const bool wide = copy_avx512();
-        const size_t body = n & ~static_cast<size_t>(wide ? 127 : 63);
-        if (wide)
-            stream_lines_avx512(dst, src, body);
-        else
-            stream_lines_sse(dst, src, body);
+        const size_t body = n & ~size_t{63};
+        for (size_t i = 0; i < body; i += 64) {
+            const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+            const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+            const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+            const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+        }
         dst += body;
         src += body;
         n -= body;
@@ -211,16 +181,6 @@ private:
     std::map<size_t, std::vector<void*>> free_;
     size_t free_bytes_ = 0;
 };
-
-// Streams a direct batch spreads its per-unit DMAs over (ELECT_EC_DIRECT_STREAMS, 1 or 2).
-int direct_streams()
-{
-    static const int n = [] {
-        const char* e = std::getenv("ELECT_EC_DIRECT_STREAMS");
-        return e && std::atoi(e) == 1 ? 1 : 2;
-    }();
-    return n;
-}
 
 // Every byte the call reads and writes lies in page-locked pool buffers.
 bool direct_op(const HostOp& op, size_t len)
@@ -807,9 +767,6 @@ private:
         std::condition_variable done;  // this batch's callers wait here for kDone
         hipStream_t stream = nullptr;
         hipEvent_t h2d_done = nullptr;
-        // direct batches: a second stream for half of the per-unit DMAs, and its fork/join events
-        hipStream_t stream2 = nullptr;
-        hipEvent_t fork = nullptr, join = nullptr;
 
         Shape shape() const
         {
@@ -865,9 +822,6 @@ private:
             s.owner = this;
             hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming);
-            if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream2, hipStreamNonBlocking);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&s.fork, hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&s.join, hipEventDisableTiming);
             // device first: an arena too large for the device fails there, before any host pinning
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_in), arena);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_out), arena);
@@ -895,9 +849,6 @@ private:
         for (Slab& s : active()) {
             if (s.stream) (void)hipStreamDestroy(s.stream);
             if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
-            if (s.stream2) (void)hipStreamDestroy(s.stream2);
-            for (hipEvent_t ev : {s.fork, s.join})
-                if (ev) (void)hipEventDestroy(ev);
             for (uint8_t* h : {s.pin_in, s.pin_out})
                 if (h) (void)hipHostFree(h);
             for (void* h : {static_cast<void*>(s.pin_lens), static_cast<void*>(s.pin_hash)})
@@ -907,8 +858,6 @@ private:
                 if (d) (void)hipFree(d);
             s.stream = nullptr;
             s.h2d_done = nullptr;
-            s.stream2 = nullptr;
-            s.fork = s.join = nullptr;
             s.pin_in = s.pin_out = s.d_in = s.d_out = nullptr;
             s.pin_lens = s.d_lens = nullptr;
             s.pin_hash = s.d_hash = nullptr;
@@ -951,10 +900,7 @@ private:
             const int n = s->reserved;
             lock.unlock();
             const hipError_t e = issue(*s, shape, n);
-            if (e != hipSuccess) {  // no callback was queued: drain both streams before the callers get their buffers back
-                (void)hipStreamSynchronize(s->stream);
-                (void)hipStreamSynchronize(s->stream2);
-            }
+            if (e != hipSuccess) (void)hipStreamSynchronize(s->stream);  // no callback was queued
             lock.lock();
             if (e != hipSuccess) finish(s, map_hip(e));
             prev = s;
@@ -968,30 +914,16 @@ private:
         const size_t in_stride = sh.tiles * sh.cols * sh.pitch;  // per slot
         const size_t out_stride = sh.tiles * sh.rows * sh.pitch;
         hipError_t e = hipSuccess;
-        // direct batches spread their per-unit DMAs over two streams, slot by slot
-        // (forked from and joined back into the slab's stream)
-        const bool two = sh.direct && direct_streams() > 1;
-        auto lane = [&](int q) { return two && (q & 1) ? s.stream2 : s.stream; };
-        auto fork = [&]() {
-            hipError_t r = hipEventRecord(s.fork, s.stream);
-            if (r == hipSuccess) r = hipStreamWaitEvent(s.stream2, s.fork, 0);
-            return r;
-        };
-        auto join = [&]() {
-            hipError_t r = hipEventRecord(s.join, s.stream2);
-            if (r == hipSuccess) r = hipStreamWaitEvent(s.stream, s.join, 0);
-            return r;
-        };
+        // Direct batches: one DMA per unit, on the slab's one stream (spreading them
+        // over two streams lost 6-8 GiB/s at 16 and 64 callers, profiles/r04/direct_streams_ab.txt).
         if (sh.direct) {  // every unit straight from its caller's page-locked buffer
-            if (two) e = fork();
             for (int q = 0; q < n && e == hipSuccess; ++q)
                 for (int j = 0; j < sh.cols && e == hipSuccess; ++j) {
                     const size_t i = static_cast<size_t>(q) * kern::kMaxCols + j;
                     if (s.dsrc_n[i])
                         e = hipMemcpyAsync(s.d_in + q * in_stride + j * sh.pitch, s.dsrc[i], s.dsrc_n[i],
-                                           hipMemcpyHostToDevice, lane(q));
+                                           hipMemcpyHostToDevice, s.stream);
                 }
-            if (two && e == hipSuccess) e = join();
         } else {
             e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
         }
@@ -1029,12 +961,10 @@ private:
             e = kern::launch_apply(p, s.stream);
         }
         if (e == hipSuccess && sh.direct) {
-            if (two) e = fork();
             for (int q = 0; q < n && e == hipSuccess; ++q)
                 for (int r = 0; r < sh.rows && e == hipSuccess; ++r)
                     e = hipMemcpyAsync(s.ddst[static_cast<size_t>(q) * kern::kMaxRows + r], s.d_out + q * out_stride + r * sh.pitch,
-                                       sh.len, hipMemcpyDeviceToHost, lane(q));
-            if (two && e == hipSuccess) e = join();
+                                       sh.len, hipMemcpyDeviceToHost, s.stream);
         } else if (e == hipSuccess) {
             e = hipMemcpyAsync(s.pin_out, s.d_out, n * out_stride, hipMemcpyDeviceToHost, s.stream);
         }

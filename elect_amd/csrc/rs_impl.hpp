@@ -145,6 +145,31 @@ __device__ __forceinline__ void store_nt(uint8_t* p, const uint4& v)
     __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
 }
 
+constexpr int kAuxNT = 2;  // buffer / LDS-DMA op cache policy: nt (gfx940 family CPol)
+
+// LDS-DMA (global_load_lds_dwordx4): lane i's 16 bytes at p land at lds + 16 i;
+// lds is wave-uniform.  The data is in LDS after the wave's vmcnt drains.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) const void* global_ptr_t;
+
+__device__ __forceinline__ void load_to_lds_nt(const uint8_t* p, uint8_t* lds)
+{
+    __builtin_amdgcn_global_load_lds((global_ptr_t)p, (lds_ptr_t)lds, 16, 0, kAuxNT);
+}
+
+// One-wave blocks only: each of the K columns' 1 KiB for the wave goes through
+// stage (K KiB of LDS), then every lane reads its 16 bytes back.
+template <int K>
+__device__ __forceinline__ void load_columns_via_lds(const uint8_t* const (&src)[K], uint8_t* stage, uint4 (&x)[K])
+{
+#pragma unroll
+    for (int j = 0; j < K; ++j) load_to_lds_nt(src[j], stage + j * 1024);
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = *reinterpret_cast<const uint4*>(stage + j * 1024 + lane * 16);
+}
+
 // Partial segments (padded launches only): n < 16 valid bytes, zero filled.
 __device__ __forceinline__ uint4 load_partial(const uint8_t* p, uint32_t n)
 {
@@ -463,10 +488,11 @@ __device__ __forceinline__ void stage_tables(const gf::PermTable (&tab)[R][K], u
 // HASH instances (encode shapes only) carry the parity-hash epilogue; keeping
 // it out of the others saved RS(12,8) encode ~120 v_mov (acc kept live across
 // the stores) and 4 VGPRs.
-template <int K, int R, bool PAD, bool HASH>
+template <int K, int R, bool PAD, bool HASH, bool LDSDMA = false>
 __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[LDSDMA ? K * 1024 : 16];  // (LDSDMA: one-wave blocks)
     const uint32_t idx_raw = blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = idx_raw < a.total;
     // Lanes past the end of the launch redo the last segment (identical bytes
@@ -493,7 +519,12 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 
     stage_tables<K, R>(a.tab, tl);
     if (HASH ? first >= a.total : !live) return;  // HASH: only wholly dead waves leave
-    if (!PAD) {
+    if constexpr (!PAD && LDSDMA) {
+        const uint8_t* src[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) src[j] = a.sp[j] + stripe * a.ss[j] + off;
+        load_columns_via_lds<K>(src, stage, x);
+    } else if (!PAD) {
 #pragma unroll
         for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + stripe * a.ss[j] + off);
     }
@@ -600,10 +631,11 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
 // RS(12,8) encode, 15 in RS(6,4) encode).
 // HASH: every wave lies inside one hashed unit, so it writes one partial per
 // row (hash_reduce reads it in either mode: no wave starts outside its unit).
-template <int K, int R, bool HASH>
+template <int K, int R, bool HASH, bool LDSDMA = false>
 __global__ __launch_bounds__(kBlock) void gf_apply_x16u(const FastArgs<K, R> a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[LDSDMA ? K * 1024 : 16];  // (LDSDMA: one-wave blocks)
     const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t first = __builtin_amdgcn_readfirstlane(idx);  // the wave's lane 0
     const uint32_t stripe = div_magic(first, a.magic, a.shift);  // wave-uniform
@@ -611,8 +643,15 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16u(const FastArgs<K, R> a)
     stage_tables<K, R>(a.tab, tl);
     if (first >= a.total) return;  // total % 64 == 0: waves are wholly live or wholly past the end
     uint4 x[K];
+    if constexpr (LDSDMA) {
+        const uint8_t* src[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + static_cast<uint64_t>(stripe) * a.ss[j] + off);
+        for (int j = 0; j < K; ++j) src[j] = a.sp[j] + static_cast<uint64_t>(stripe) * a.ss[j] + off;
+        load_columns_via_lds<K>(src, stage, x);
+    } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + static_cast<uint64_t>(stripe) * a.ss[j] + off);
+    }
     uint4 acc[R];
     gf_combine<K, R>(x, tl, acc);
 #pragma unroll
@@ -638,7 +677,6 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16u(const FastArgs<K, R> a)
 // overlapped with the table staging.  The one segment per unit that straddles
 // its content length is loaded whole (it lies inside the unit's L bytes) and
 // masked, so no byte loads.  Straddling waves take a one-segment-at-a-time path.
-constexpr int kAuxNT = 2;  // buffer op cache policy: nt (gfx940 family CPol)
 
 template <int K, int R, int U>
 __global__ __launch_bounds__(kBlock) void gf_apply_lens(const FastArgs<K, R> a)
@@ -876,10 +914,19 @@ struct LaunchPolicy {
     // The parity update gf_update_x16: 81.6 -> 84.2 % (plain_one_wave_ab.txt)
     int update_block = 64;
     int update_waves = 18;
-    // Scalar stripe bases (gf_apply_x16u, the grouped kernel's UNI form) for plain launches
-    // of whole-wave stripes with at least this many columns: RS(12,8) two-erasure decode
-    // 79.9 -> 81.6 %; four-column shapes lose 0.5 % with them (profiles/r02_scalarbase_ab/)
-    int scalar_base_min_cols = 8;
+    // Scalar stripe bases (gf_apply_x16u) for plain launches of whole-wave stripes with at
+    // least this many columns: RS(12,8) two-erasure decode 79.9 -> 81.6 % (round 2,
+    // profiles/r02_scalarbase_ab/, where four-column shapes lost 0.5 % with 256-thread blocks);
+    // in one-wave blocks four-column shapes gain too: the headline step 4,511-4,521 ->
+    // 4,522-4,528 GiB/s, RS(6,4) decode 84.7-84.9 -> 85.0-85.1 % (round 4, profiles/r04/policy_ab.txt)
+    int scalar_base_min_cols = 4;
+    // ... and for the grouped kernel's UNI form: from 4 columns the mixed config lost 1 %
+    // (4,549-4,571 -> 4,507-4,538 GiB/s, policy_ab.txt)
+    int group_scalar_base_min_cols = 8;
+    // Plain one-wave launches load their columns through LDS (global_load_lds_dwordx4, the
+    // LDS-DMA path, then ds_read_b128) instead of into VGPRs: the XOR-only encode pattern
+    // ran 0.8-0.9 points faster that way (profiles/r04/lds_dma_probe.txt).
+    bool plain_lds_dma = false;
 };
 
 #ifdef ELECT_EC_POLICY_HEADER
@@ -951,7 +998,11 @@ inline size_t cap_lds(int block, int coefs, int waves)
     return per_block > static_lds ? per_block - static_lds : 0;
 }
 
-inline size_t cap_lds(const LaunchShape& sh, int coefs) { return cap_lds(sh.block, coefs, sh.waves); }
+inline size_t cap_lds(const LaunchShape& sh, int coefs, size_t extra_static = 0)
+{
+    const size_t d = cap_lds(sh.block, coefs, sh.waves);
+    return d > extra_static ? d - extra_static : 0;
+}
 
 // Padded launches the per-stripe-length kernel can take (whole 16-byte segments,
 // aligned columns).  (Hashed launches do not: a hashed form of gf_apply_lens
@@ -1048,8 +1099,18 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             const size_t lds = cap_lds(sh, kCoefs);
             if (!a.hashes) {
                 bool launched = false;
-                if constexpr (K >= kPolicy.scalar_base_min_cols) {  // (scalar-base plain instances: wide shapes only)
-                    if (scalar_base) {
+                if constexpr (kPolicy.plain_lds_dma) {  // one-wave launches load through LDS
+                    if (sh.block == 64) {
+                        const size_t lds_d = cap_lds(sh, kCoefs, K * 1024);
+                        if (scalar_base && K >= kPolicy.scalar_base_min_cols)
+                            hipLaunchKernelGGL((gf_apply_x16u<K, R, false, true>), grid, dim3(sh.block), lds_d, stream, a);
+                        else
+                            hipLaunchKernelGGL((gf_apply_x16<K, R, false, false, true>), grid, dim3(sh.block), lds_d, stream, a);
+                        launched = true;
+                    }
+                }
+                if constexpr (K >= kPolicy.scalar_base_min_cols) {  // (the scalar-base plain instances)
+                    if (!launched && scalar_base) {
                         hipLaunchKernelGGL((gf_apply_x16u<K, R, false>), grid, dim3(sh.block), lds, stream, a);
                         launched = true;
                     }
@@ -1124,7 +1185,7 @@ hipError_t launch_group_kr(const ApplyParams* ps, int n, int r0, hipStream_t str
     }
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const size_t lds = cap_lds(sh, R * K);
-    if (uni && K >= kPolicy.scalar_base_min_cols)
+    if (uni && K >= kPolicy.group_scalar_base_min_cols)
         hipLaunchKernelGGL((gf_apply_group<K, R, true>), dim3(static_cast<uint32_t>(blocks)), dim3(block), lds, stream, a);
     else
         hipLaunchKernelGGL((gf_apply_group<K, R, false>), dim3(static_cast<uint32_t>(blocks)), dim3(block), lds, stream, a);
