@@ -923,10 +923,12 @@ struct LaunchPolicy {
     // ... and for the grouped kernel's UNI form: from 4 columns the mixed config lost 1 %
     // (4,549-4,571 -> 4,507-4,538 GiB/s, policy_ab.txt)
     int group_scalar_base_min_cols = 8;
-    // Plain one-wave launches load their columns through LDS (global_load_lds_dwordx4, the
-    // LDS-DMA path, then ds_read_b128) instead of into VGPRs: the XOR-only encode pattern
-    // ran 0.8-0.9 points faster that way (profiles/r04/lds_dma_probe.txt).
-    bool plain_lds_dma = false;
+    // Plain one-wave launches that load their columns through LDS (global_load_lds_dwordx4,
+    // the LDS-DMA path, then ds_read_b128) instead of into VGPRs: 0 none, 1 read-heavy ones
+    // (decodes), 2 all.  The XOR-only encode pattern ran 0.8-0.9 points faster that way
+    // (profiles/r04/lds_dma_probe.txt); in the product, all: RS(6,4) encode 84.15 -> 83.8 %,
+    // decode 84.2-84.5 -> 84.7-85.0 % (profiles/r04/lds_dma_ab.txt).
+    int plain_lds_dma = 0;
 };
 
 #ifdef ELECT_EC_POLICY_HEADER
@@ -1099,8 +1101,8 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             const size_t lds = cap_lds(sh, kCoefs);
             if (!a.hashes) {
                 bool launched = false;
-                if constexpr (kPolicy.plain_lds_dma) {  // one-wave launches load through LDS
-                    if (sh.block == 64) {
+                if constexpr (kPolicy.plain_lds_dma > 0) {  // one-wave launches load through LDS
+                    if (sh.block == 64 && (kPolicy.plain_lds_dma > 1 || 2 * R < K)) {
                         const size_t lds_d = cap_lds(sh, kCoefs, K * 1024);
                         if (scalar_base && K >= kPolicy.scalar_base_min_cols)
                             hipLaunchKernelGGL((gf_apply_x16u<K, R, false, true>), grid, dim3(sh.block), lds_d, stream, a);
