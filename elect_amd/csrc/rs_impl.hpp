@@ -927,8 +927,9 @@ struct LaunchPolicy {
     // the LDS-DMA path, then ds_read_b128) instead of into VGPRs: 0 none, 1 read-heavy ones
     // (decodes), 2 all.  The XOR-only encode pattern ran 0.8-0.9 points faster that way
     // (profiles/r04/lds_dma_probe.txt); in the product, all: RS(6,4) encode 84.15 -> 83.8 %,
-    // decode 84.2-84.5 -> 84.7-85.0 % (profiles/r04/lds_dma_ab.txt).
-    int plain_lds_dma = 0;
+    // decode 84.2-84.5 -> 84.7-85.0 %; read-heavy only: the headline step 4,507-4,511 ->
+    // 4,516-4,520 GiB/s, decode 84.5-84.9 -> 85.1-85.2 %, encode unchanged (profiles/r04/lds_dma_ab.txt).
+    int plain_lds_dma = 1;
 };
 
 #ifdef ELECT_EC_POLICY_HEADER
