@@ -268,6 +268,26 @@ for step in "$@"; do
             ELECT_EC_COPY_ISA=$isa run "copyisa_${isa}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
                 --host-seconds ${HOST_S:-2} || exit $?
         done; done; done ;;
+    final)  # the round's judged artefacts: GPU suite, smoke, the driver's bench command, rocprof stats, PMC traffic,
+            # the BASELINE configs and the fused steps (collect with tools/collect_final.sh)
+        run pytest_gpu 1000 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+        rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+        run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+        run bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $?
+        run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run \
+            -- python3 bench.py --no-cpu --no-host --no-sizes --no-configs --steps 50 --warmup 5 || exit $?
+        run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_$TAG -o run \
+            -- python3 bench.py --no-cpu --no-host --no-sizes --no-configs --steps 5 --warmup 1 || exit $?
+        run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$TAG -o run \
+            -- python3 bench.py --no-cpu --no-host --no-sizes --no-configs --steps 5 --warmup 1 || exit $?
+        run cfg_mixed 400 python bench.py --config mixed || exit $?
+        run cfg_rs12 400 python bench.py --config rs12 || exit $?
+        run cfg_update 400 python bench.py --config update || exit $?
+        run cfg_padded 400 python bench.py --config padded || exit $?
+        run cfg_hashed 400 python bench.py --config hashed || exit $?
+        run cfg_flows_elect 400 python bench.py --config flows --chunk 4404020 --stripes 256 || exit $?
+        run cfg_hostpath_T64 400 python bench.py --config hostpath --threads 64 --host-seconds 2 || exit $?
+        run cfg_hostpath_T64_pinned 400 python bench.py --config hostpath --threads 64 --host-seconds 2 --host-alloc pinned || exit $? ;;
     padfill)  # padded encode vs content fill: where the time goes
         for f in 1.0 0.0 0.5 random; do
             run "bench_padded_fill_$f" 300 python bench.py --config padded --pad-fill $f || exit $?
