@@ -173,17 +173,19 @@ def max_over_ranks(x: float, world: int) -> float:
     return dist.max_over_ranks(x, world, "cuda")
 
 
-def pmc_traffic(kernel_substr: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
+def pmc_traffic(*kernel_substrs: str):
+    """HBM bytes per launch from the newest committed rocprofv3 PMC summary
+    (tools/pmc_traffic.py) that has one of the named kernels."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
         except Exception:
             continue
-        for name, rec in d.get("kernels", {}).items():
-            if kernel_substr in name:
-                return rec.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+        for sub in kernel_substrs:
+            for name, rec in d.get("kernels", {}).items():
+                if sub in name:
+                    return rec.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -1520,7 +1522,8 @@ def main():
     dec_alg = B * (k + 1) * L         # (k+e)*L per stripe, e = 1
     enc_gbs = enc_alg / (enc_ms * 1e-3) / 1e9
     dec_gbs = dec_alg / (dec_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic("gf_apply_x16<4, 2")
+    # the encode launch: the scalar-base kernel since round 4 (one-wave blocks, whole-wave stripes)
+    traffic, traffic_src = pmc_traffic("gf_apply_x16u<4, 2, false, false>", "gf_apply_x16<4, 2")
 
     out = {
         "metric": f"GiB/s device-resident RS({n},{k}) encode+decode, {chunk_name(L)} chunks, 1/2/4/8 GPU",
@@ -1554,7 +1557,7 @@ def main():
             "unit": "GB/s",
             "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "gf_apply_x16<4,2> (encode)",
+            "kernel": "gf_apply_x16u<4,2> (encode)",
             "algorithmic_bytes_per_launch": enc_alg,
             "traffic_source": traffic_src,
         },
