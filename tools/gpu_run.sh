@@ -72,6 +72,11 @@ for step in "$@"; do
         run bench_rehearse_2rank 600 python bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu || exit $?
         run bench_rehearse_2rank_mixed 600 python bench.py --gpus 2 --config mixed --steps 10 || exit $?
         unset ELECT_BENCH_SHARE_GPU ;;
+    rehearse)  # the driver's multi-GPU commands with every rank on the one GPU (round 4: with the pinned host-path child)
+        export ELECT_BENCH_SHARE_GPU=1
+        run rehearse_2rank 600 python bench.py --gpus 2 --steps 20 --warmup 5 || exit $?
+        run rehearse_8rank 900 python bench.py --gpus 8 --steps 20 --warmup 5 || exit $?
+        unset ELECT_BENCH_SHARE_GPU ;;
     multirank8)  # the 8-rank plumbing on the one GPU (gloo; every rank's kernels share the device)
         export ELECT_BENCH_SHARE_GPU=1
         run bench_rehearse_8rank 600 python bench.py --gpus 8 --steps 10 --warmup 2 --no-cpu --no-host --rotate 2 || exit $?
