@@ -74,6 +74,86 @@ namespace {
 
 constexpr int kBlock = 256;
 
+// ---------------------------------------------------------------------------
+// Launch policy: the block size and the occupancy cap of every launch.
+//
+// The cap is the number of the launch's waves resident per CU (0: uncapped),
+// set with dynamic LDS that no block reads (cap_lds: 160 KiB per CU / blocks).
+// Fewer waves in flight keep fewer HBM pages open: an uncapped RS(6,4) decode
+// waits on DRAM read credits 6x as often (profiles/r02_pmc_occupancy_ab.txt).
+// One-wave blocks let the cap move in single waves; the best points (18 waves
+// for RS(6,4), 12 for RS(12,8) decodes) lie two waves above cliffs where the
+// rate falls by several points.  Every entry was chosen by interleaved A/B
+// runs of the product library; the evidence file is named beside it, and
+// DESIGN.md §4 has the launch-shape table.  A/B builds swap the whole table
+// (tools/ab_build.sh NAME -DELECT_EC_POLICY_HEADER='"file.hpp"'); the product
+// compiles this one.
+// ---------------------------------------------------------------------------
+struct LaunchPolicy {
+    // Plain launches (no padding, no hash): gf_apply_x16 / gf_apply_x16u.
+    uint64_t small_len = 4096;       // chunks up to this run 128-thread blocks (round 1: +3-4 % over 256)
+    int small_block = 128;
+    // > 4 KiB and < 16 coefficients: one-wave blocks (profiles/r03/plain_one_wave_ab.txt: RS(6,4)
+    // encode 82.5 -> 84.1 %, decode 81.6 -> 83.8 %, RS(12,8) one-erasure decode 79.0 -> 84.8 %)
+    int one_wave_write_waves = 18;   // write-heavy (2R >= K): RS(6,4) encode (14: 82.0 %, 12: 75.7 %)
+    int one_wave_read_waves = 18;    // read-heavy, < 8 columns: RS(6,4) decode (15: 80.7 %)
+    int one_wave_read_wide_waves = 12;  // read-heavy, >= 8 columns: RS(12,8) one-erasure decode
+    // >= 16 coefficients, and chunks <= 4 KiB
+    int wide_write_block = 256;      // RS(12,8) encode: 64 / 128 / 256 threads 75.5 / 73.9 / 76.8 % (block_wide_ab.txt)
+    int wide_read_block = 128;       // RS(12,8) decodes (64: the same; 256: 78 against 85 %)
+    int write_waves = 24;            // profiles/r02_occupancy_ab/ (RS(12,8) encode at 16 / 12: 72.5 / 66.9 %)
+    int read_waves = 20;             // profiles/r02_occupancy_ab/ (1 KiB decodes at 16 / 24: 80.7 / 81.4 vs 82.4 %)
+    int read_wide_waves = 12;        // >= 8 columns and >= 2 rows: RS(12,8) two-erasure decode at 20 / 16 / 14 /
+                                     // 12 / 10 waves 78.2 / 79.5 / 83.0 / 85.2 / 75.7 % (occupancy_wide_ab.txt)
+    // Plain launches with the parity hash (the fused-hash encode): one-wave blocks;
+    // the scalar-base form capped at 20 waves (80.7 -> 81.2 %, plain_one_wave_ab.txt),
+    // the per-lane form uncapped (caps of 24 / 28 cost 5 / 3 points, profiles/r02_hash_ab/)
+    int hashed_block = 64;
+    int hashed_scalar_waves = 20;
+    int hashed_lane_waves = 0;
+    int hashed_scalar_base_min_cols = 1;  // hashed launches take the scalar-base form from this width up
+    // Padded launches: gf_apply_x16<PAD> (uncapped) and gf_apply_lens (capped).
+    int padded_write_block = 128;    // random fill 68.9 -> 71.8 %, full 82.3 -> 82.7 % (block_pad_ab.txt);
+                                     // read-heavy ones keep the plain block (64 / 128: -3 / -4 points)
+    int lens_write_waves = 24;       // gf_apply_lens: degraded read 76.4 -> 77.4 % at 20 (profiles/r02_lenscap_ab/)
+    int lens_read_waves = 20;
+    // Padded launches with the hash (ELECT's fused encode and update steps): one-wave
+    // blocks, uncapped (79.6 -> 81.0 % at ELECT's codeLength; caps of 20-28 lose:
+    // block_hash_pad_ab.txt)
+    int padded_hashed_block = 64;
+    // Grouped launches (the mixed config): one-wave blocks with the plain caps of their
+    // shape (8-way share 4,198 -> 4,397 GiB/s; group_small_block_ab.txt, plain_one_wave_ab.txt)
+    int group_block = 64;
+    // The parity update gf_update_x16: 81.6 -> 84.2 % (plain_one_wave_ab.txt)
+    int update_block = 64;
+    int update_waves = 18;
+    // Scalar stripe bases (gf_apply_x16u) for plain launches of whole-wave stripes with at
+    // least this many columns: RS(12,8) two-erasure decode 79.9 -> 81.6 % (round 2,
+    // profiles/r02_scalarbase_ab/, where four-column shapes lost 0.5 % with 256-thread blocks);
+    // in one-wave blocks four-column shapes gain too: the headline step 4,511-4,521 ->
+    // 4,522-4,528 GiB/s, RS(6,4) decode 84.7-84.9 -> 85.0-85.1 % (round 4, profiles/r04/policy_ab.txt)
+    int scalar_base_min_cols = 4;
+    // ... and for the grouped kernel's UNI form: from 4 columns the mixed config lost 1 %
+    // (4,549-4,571 -> 4,507-4,538 GiB/s, policy_ab.txt)
+    int group_scalar_base_min_cols = 8;
+    // Plain one-wave launches that load their columns through LDS (global_load_lds_dwordx4,
+    // the LDS-DMA path, then ds_read_b128) instead of into VGPRs: 0 none, 1 read-heavy ones
+    // (decodes), 2 all.  The XOR-only encode pattern ran 0.8-0.9 points faster that way
+    // (profiles/r04/lds_dma_probe.txt); in the product, all: RS(6,4) encode 84.15 -> 83.8 %,
+    // decode 84.2-84.5 -> 84.7-85.0 %; read-heavy only: the headline step 4,507-4,511 ->
+    // 4,516-4,520 GiB/s, decode 84.5-84.9 -> 85.1-85.2 %, encode unchanged (profiles/r04/lds_dma_ab.txt).
+    int plain_lds_dma = 1;
+    // The parity hash's per-wave sum weights each lane by 31^(16 lane) inside a DPP tree
+    // (wave_poly31) instead of a per-lane table load that waits behind the parity stores.
+    bool hash_dpp_weights = false;
+};
+
+#ifdef ELECT_EC_POLICY_HEADER
+#include ELECT_EC_POLICY_HEADER  // defines kPolicy (A/B builds only)
+#else
+constexpr LaunchPolicy kPolicy{};
+#endif
+
 // q = (n * m) >> p is exact floor(n / d) for every n < 2^31 (m = ceil(2^p/d),
 // p = 31 + ceil(log2 d); the rounding error m*d - 2^p < d keeps n*err < 2^p).
 struct Magic {
@@ -293,6 +373,47 @@ template <int Ctrl, int RowMask = 0xF>
 __device__ __forceinline__ uint32_t dpp_add(uint32_t v)
 {
     return v + static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), Ctrl, RowMask, 0xF, false));
+}
+
+// Sum over the 64 lanes of v_l * 31^(16 l) (lane l's 16 bytes follow lane l-1's),
+// returned wave-uniform, with no per-lane weight table: a DPP tree where each
+// level adds the partner 2^i lanes up, weighted by 31^(16 * 2^i) (row_shl
+// within 16-lane rows, then the four rows' sums read out and combined in SALU).
+// The table form (kLanePow[lane] * v, then wave_sum) loads the weight per lane
+// after the parity stores, and on gfx9 vmcnt counts those stores too: every
+// wave's epilogue waited for its own stores to land.
+template <int Ctrl>
+__device__ __forceinline__ uint32_t dpp_read(uint32_t v)  // bound_ctrl: 0 for lanes past the row
+{
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), Ctrl, 0xF, 0xF, true));
+}
+
+struct Pow31Lanes {  // 31^(16 * n) for n = 1, 2, 4, 8, 16, 32, 48
+    uint32_t b1, b2, b4, b8, b16, b32, b48;
+    constexpr Pow31Lanes() : b1(1), b2(0), b4(0), b8(0), b16(0), b32(0), b48(0)
+    {
+        for (int i = 0; i < 16; ++i) b1 *= 31u;
+        b2 = b1 * b1;
+        b4 = b2 * b2;
+        b8 = b4 * b4;
+        b16 = b8 * b8;
+        b32 = b16 * b16;
+        b48 = b32 * b16;
+    }
+};
+
+__device__ __forceinline__ uint32_t wave_poly31(uint32_t v)
+{
+    constexpr Pow31Lanes kP{};
+    v += kP.b1 * dpp_read<0x101>(v);  // row_shl:1
+    v += kP.b2 * dpp_read<0x102>(v);  // row_shl:2
+    v += kP.b4 * dpp_read<0x104>(v);  // row_shl:4
+    v += kP.b8 * dpp_read<0x108>(v);  // row_shl:8: lane 16 r holds row r's weighted sum
+    const uint32_t r0 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 0));
+    const uint32_t r1 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 16));
+    const uint32_t r2 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 32));
+    const uint32_t r3 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 48));
+    return r0 + kP.b16 * r1 + kP.b32 * r2 + kP.b48 * r3;
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
@@ -595,10 +716,13 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         if (whole_wave) {  // partial sums to scratch; hash_reduce adds them per stripe
             const uint32_t seg0 = first - s_first * a.hsegs;
             const uint32_t p0 = a.hpow * pow31_seg(seg0);
-            const uint32_t q = kLanePow.v[threadIdx.x & 63u] * p0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const uint32_t sum = wave_sum(horner31(acc[r]) * q);
+                uint32_t sum;
+                if constexpr (kPolicy.hash_dpp_weights)
+                    sum = p0 * wave_poly31(horner31(acc[r]));
+                else
+                    sum = wave_sum(horner31(acc[r]) * (kLanePow.v[threadIdx.x & 63u] * p0));
                 if ((threadIdx.x & 63u) == 0) a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum;
             }
         } else if (a.hpart_hi) {  // assign mode: a wave straddling two stripes (or the launch's end)
@@ -659,10 +783,14 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16u(const FastArgs<K, R> a)
     if constexpr (HASH) {
         if (a.hashes) {
             const uint32_t hs = div_magic(first, a.hmagic, a.hshift);
-            const uint32_t q = kLanePow.v[threadIdx.x & 63u] * (a.hpow * pow31_seg(first - hs * a.hsegs));
+            const uint32_t p0 = a.hpow * pow31_seg(first - hs * a.hsegs);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const uint32_t sum = wave_sum(horner31(acc[r]) * q);
+                uint32_t sum;
+                if constexpr (kPolicy.hash_dpp_weights)
+                    sum = p0 * wave_poly31(horner31(acc[r]));
+                else
+                    sum = wave_sum(horner31(acc[r]) * (kLanePow.v[threadIdx.x & 63u] * p0));
                 if ((threadIdx.x & 63u) == 0) a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum;
             }
         }
@@ -861,82 +989,6 @@ constexpr int lens_unroll() { return K <= 4 ? 2 : 1; }
     }
 }
 
-// ---------------------------------------------------------------------------
-// Launch policy: the block size and the occupancy cap of every launch.
-//
-// The cap is the number of the launch's waves resident per CU (0: uncapped),
-// set with dynamic LDS that no block reads (cap_lds: 160 KiB per CU / blocks).
-// Fewer waves in flight keep fewer HBM pages open: an uncapped RS(6,4) decode
-// waits on DRAM read credits 6x as often (profiles/r02_pmc_occupancy_ab.txt).
-// One-wave blocks let the cap move in single waves; the best points (18 waves
-// for RS(6,4), 12 for RS(12,8) decodes) lie two waves above cliffs where the
-// rate falls by several points.  Every entry was chosen by interleaved A/B
-// runs of the product library; the evidence file is named beside it, and
-// DESIGN.md §4 has the launch-shape table.  A/B builds swap the whole table
-// (tools/ab_build.sh NAME -DELECT_EC_POLICY_HEADER='"file.hpp"'); the product
-// compiles this one.
-// ---------------------------------------------------------------------------
-struct LaunchPolicy {
-    // Plain launches (no padding, no hash): gf_apply_x16 / gf_apply_x16u.
-    uint64_t small_len = 4096;       // chunks up to this run 128-thread blocks (round 1: +3-4 % over 256)
-    int small_block = 128;
-    // > 4 KiB and < 16 coefficients: one-wave blocks (profiles/r03/plain_one_wave_ab.txt: RS(6,4)
-    // encode 82.5 -> 84.1 %, decode 81.6 -> 83.8 %, RS(12,8) one-erasure decode 79.0 -> 84.8 %)
-    int one_wave_write_waves = 18;   // write-heavy (2R >= K): RS(6,4) encode (14: 82.0 %, 12: 75.7 %)
-    int one_wave_read_waves = 18;    // read-heavy, < 8 columns: RS(6,4) decode (15: 80.7 %)
-    int one_wave_read_wide_waves = 12;  // read-heavy, >= 8 columns: RS(12,8) one-erasure decode
-    // >= 16 coefficients, and chunks <= 4 KiB
-    int wide_write_block = 256;      // RS(12,8) encode: 64 / 128 / 256 threads 75.5 / 73.9 / 76.8 % (block_wide_ab.txt)
-    int wide_read_block = 128;       // RS(12,8) decodes (64: the same; 256: 78 against 85 %)
-    int write_waves = 24;            // profiles/r02_occupancy_ab/ (RS(12,8) encode at 16 / 12: 72.5 / 66.9 %)
-    int read_waves = 20;             // profiles/r02_occupancy_ab/ (1 KiB decodes at 16 / 24: 80.7 / 81.4 vs 82.4 %)
-    int read_wide_waves = 12;        // >= 8 columns and >= 2 rows: RS(12,8) two-erasure decode at 20 / 16 / 14 /
-                                     // 12 / 10 waves 78.2 / 79.5 / 83.0 / 85.2 / 75.7 % (occupancy_wide_ab.txt)
-    // Plain launches with the parity hash (the fused-hash encode): one-wave blocks;
-    // the scalar-base form capped at 20 waves (80.7 -> 81.2 %, plain_one_wave_ab.txt),
-    // the per-lane form uncapped (caps of 24 / 28 cost 5 / 3 points, profiles/r02_hash_ab/)
-    int hashed_block = 64;
-    int hashed_scalar_waves = 20;
-    int hashed_lane_waves = 0;
-    int hashed_scalar_base_min_cols = 1;  // hashed launches take the scalar-base form from this width up
-    // Padded launches: gf_apply_x16<PAD> (uncapped) and gf_apply_lens (capped).
-    int padded_write_block = 128;    // random fill 68.9 -> 71.8 %, full 82.3 -> 82.7 % (block_pad_ab.txt);
-                                     // read-heavy ones keep the plain block (64 / 128: -3 / -4 points)
-    int lens_write_waves = 24;       // gf_apply_lens: degraded read 76.4 -> 77.4 % at 20 (profiles/r02_lenscap_ab/)
-    int lens_read_waves = 20;
-    // Padded launches with the hash (ELECT's fused encode and update steps): one-wave
-    // blocks, uncapped (79.6 -> 81.0 % at ELECT's codeLength; caps of 20-28 lose:
-    // block_hash_pad_ab.txt)
-    int padded_hashed_block = 64;
-    // Grouped launches (the mixed config): one-wave blocks with the plain caps of their
-    // shape (8-way share 4,198 -> 4,397 GiB/s; group_small_block_ab.txt, plain_one_wave_ab.txt)
-    int group_block = 64;
-    // The parity update gf_update_x16: 81.6 -> 84.2 % (plain_one_wave_ab.txt)
-    int update_block = 64;
-    int update_waves = 18;
-    // Scalar stripe bases (gf_apply_x16u) for plain launches of whole-wave stripes with at
-    // least this many columns: RS(12,8) two-erasure decode 79.9 -> 81.6 % (round 2,
-    // profiles/r02_scalarbase_ab/, where four-column shapes lost 0.5 % with 256-thread blocks);
-    // in one-wave blocks four-column shapes gain too: the headline step 4,511-4,521 ->
-    // 4,522-4,528 GiB/s, RS(6,4) decode 84.7-84.9 -> 85.0-85.1 % (round 4, profiles/r04/policy_ab.txt)
-    int scalar_base_min_cols = 4;
-    // ... and for the grouped kernel's UNI form: from 4 columns the mixed config lost 1 %
-    // (4,549-4,571 -> 4,507-4,538 GiB/s, policy_ab.txt)
-    int group_scalar_base_min_cols = 8;
-    // Plain one-wave launches that load their columns through LDS (global_load_lds_dwordx4,
-    // the LDS-DMA path, then ds_read_b128) instead of into VGPRs: 0 none, 1 read-heavy ones
-    // (decodes), 2 all.  The XOR-only encode pattern ran 0.8-0.9 points faster that way
-    // (profiles/r04/lds_dma_probe.txt); in the product, all: RS(6,4) encode 84.15 -> 83.8 %,
-    // decode 84.2-84.5 -> 84.7-85.0 %; read-heavy only: the headline step 4,507-4,511 ->
-    // 4,516-4,520 GiB/s, decode 84.5-84.9 -> 85.1-85.2 %, encode unchanged (profiles/r04/lds_dma_ab.txt).
-    int plain_lds_dma = 1;
-};
-
-#ifdef ELECT_EC_POLICY_HEADER
-#include ELECT_EC_POLICY_HEADER  // defines kPolicy (A/B builds only)
-#else
-constexpr LaunchPolicy kPolicy{};
-#endif
 
 struct LaunchShape {
     int block;
