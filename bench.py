@@ -10,7 +10,9 @@ its own batch (weak scaling, no collective on the data path).
 value = data bytes coded by all ranks (k*L per stripe per operation) / the
 slowest rank's time, in GiB/s.  roofline = the encode kernel (dominant launch):
 algorithmic bytes (k+m)*L*B per launch / its mean HIP-event duration, against
-the 8.0 TB/s HBM3E peak.  cpu_baseline = the oracle's ISA-L-algorithm SIMD path
+the 8.0 TB/s HBM3E peak.  The timed steps issue their launches only; the
+per-launch events time the same launches in the steps right after (split_pass),
+since each event record holds the next launch back ~4 us.  cpu_baseline = the oracle's ISA-L-algorithm SIMD path
 on the host cores, rank 0 only (test infrastructure, not the product path).
 sizes = the same step and timing at the north star's other chunk sizes (1 KiB,
 1 MiB; 1 GiB of data per rank each) next to the 64 KiB line, so every
@@ -40,6 +42,67 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, decimal GB/s (MI355X_MICROARCH.md)
 GIB = float(1 << 30)
+
+HIP_EVENT_DISABLE_SYSTEM_FENCE = 0x20000000  # hip_runtime_api.h
+EVENT_RELEASE = {"device": HIP_EVENT_DISABLE_SYSTEM_FENCE, "system": 0}
+event_release = "device"  # set from --event-release in main()
+
+
+class Event:
+    """A timing HIP event on the stream the kernels run on, as Event()
+    but recorded with a device-scope release by default.  torch's timing events release to system
+    scope: every record writes back and invalidates the L2 before the next kernel may start, and
+    bench.py records three per step to split encode from decode.  That cost the headline ~6 us a
+    step (1.4 %) against the same launches with no events (tools/tune/gap_probe.py,
+    profiles/r04/event_release_ab.txt).  Nothing on the host reads what the kernels wrote
+    between two steps, so the device-scope release is all the timing needs.  The handle comes from
+    the HIP runtime torch loaded (one libamdhip64.so.7 per process), so torch's stream handles are
+    valid here."""
+    _hip = None
+
+    @classmethod
+    def hip(cls):
+        if cls._hip is None:
+            import ctypes
+            h = ctypes.CDLL("libamdhip64.so.7")
+            h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            h.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            h.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+            h.hipEventSynchronize.argtypes = [ctypes.c_void_p]
+            h.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            cls._hip = h
+        return cls._hip
+
+    def __init__(self):
+        import ctypes
+        self.h = ctypes.c_void_p()
+        rc = self.hip().hipEventCreateWithFlags(ctypes.byref(self.h), EVENT_RELEASE[event_release])
+        if rc != 0:
+            raise RuntimeError(f"hipEventCreateWithFlags: error {rc}")
+
+    def record(self, stream=None):
+        s = (stream if stream is not None else torch.cuda.current_stream()).cuda_stream
+        rc = self.hip().hipEventRecord(self.h, s)
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord: error {rc}")
+
+    def synchronize(self):
+        rc = self.hip().hipEventSynchronize(self.h)
+        if rc != 0:
+            raise RuntimeError(f"hipEventSynchronize: error {rc}")
+
+    def elapsed_time(self, end: "Event") -> float:
+        import ctypes
+        ms = ctypes.c_float()
+        rc = self.hip().hipEventElapsedTime(ctypes.byref(ms), self.h, end.h)
+        if rc != 0:
+            raise RuntimeError(f"hipEventElapsedTime: error {rc}")
+        return ms.value
+
+    def __del__(self):
+        if getattr(self, "h", None) and self._hip is not None:
+            self._hip.hipEventDestroy(self.h)
+            self.h = None
 
 
 def parse():
@@ -132,6 +195,9 @@ def parse():
                          "S > 1 consecutive steps' kernels may overlap at their boundaries")
     ap.add_argument("--graph", action="store_true",
                     help="headline and mixed: capture each step's launches in a HIP graph and replay it")
+    ap.add_argument("--event-release", choices=tuple(EVENT_RELEASE), default="device",
+                    help="scope of the release the timing events' records make: device (the default) or system "
+                         "(torch.cuda.Event's, which writes back and invalidates L2 at every record)")
     ap.add_argument("--launch-check", action="store_true",
                     help="plumbing check without a GPU: start the ranks, run the gloo handshake, print "
                          "one JSON line (tests/test_bench_launch_cpu.py)")
@@ -448,7 +514,7 @@ def decode_sweep(coder, stripe, stream, reps=5):
     for j in range(k):
         surv = [i for i in range(k + 1) if i != j]
         decode_batch(coder, stripe, surv, [j], out, inputs_by_unit=True, stream=stream)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0, e1 = Event(), Event()
         e0.record(stream)
         for _ in range(reps):
             decode_batch(coder, stripe, surv, [j], out, inputs_by_unit=True, stream=stream)
@@ -477,24 +543,24 @@ def size_sweep(args, world, rank, dev, coder, sizes=(1024, 1 << 20)):
         for _ in range(args.rotate):
             st, Bc, Lc = alloc_stripes(args, B, L, k, m, dev)
             sets.append((st, torch.empty((Bc, 1, Lc), dtype=torch.uint8, device=dev)))
-        evs = []
+        turn = [0]
+
+        def launches(i, sets=sets):
+            st, out = sets[i % len(sets)]
+            return [lambda: encode_batch(coder, st[:, :k], st[:, k:]),
+                    lambda: decode_batch(coder, st, list(range(1, k + 1)), [0], out, inputs_by_unit=True)]
 
         def step():
-            st, out = sets[len(evs) % len(sets)]
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-            e[0].record()
-            encode_batch(coder, st[:, :k], st[:, k:])
-            e[1].record()
-            decode_batch(coder, st, list(range(1, k + 1)), [0], out, inputs_by_unit=True)
-            e[2].record()
-            evs.append(e)
+            for f in launches(turn[0]):
+                f()
+            turn[0] += 1
 
-        dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms)
-        enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs[-args.steps:]) / args.steps
-        dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs[-args.steps:]) / args.steps
+        info = {}
+        dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms, info)
+        (enc_ms, dec_ms), _ = split_pass(lambda i: launches(turn[0] + i), args.steps)
         res[str(L)] = {
             "value": round(world * args.steps * 2 * B * k * L / dt / GIB, 2), "unit": "GiB/s",
-            "ms_per_step": round(dt / args.steps * 1e3, 4), "stripes_per_gpu": B,
+            "ms_per_step": round(dt / args.steps * 1e3, 4), **info, "stripes_per_gpu": B,
             "host_submit_ms_per_step": round(submit, 4),
             "layout": LAYOUT_NAMES[layout_for(args, L)],
             "encode_frac": round(B * (k + m) * L / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -510,7 +576,7 @@ def device_copy_rate(dev, nbytes=1 << 30, reps=5):
     a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     b = torch.empty_like(a)
     b.copy_(a)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0, e1 = Event(), Event()
     e0.record()
     for _ in range(reps):
         b.copy_(a)
@@ -547,7 +613,7 @@ def hbm_ceilings(dev, nbytes=1 << 31, reps=9):
             launch()
             ts = []
             for _ in range(reps):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0, e1 = Event(), Event()
                 e0.record(stream)
                 launch()
                 e1.record(stream)
@@ -624,7 +690,7 @@ def settle(step, ms: float) -> int:
     return n
 
 
-def timed(step, steps, warmup, world, settle_ms: float = 0.0):
+def timed(step, steps, warmup, world, settle_ms: float = 0.0, info: dict | None = None):
     """Warm up, then time exactly `steps` steps between barrier + synchronize on
     both sides.  Each rank's clock starts when the opening barrier releases it
     and stops at its closing synchronize (the closing gloo barrier costs ~0.6 ms
@@ -632,7 +698,10 @@ def timed(step, steps, warmup, world, settle_ms: float = 0.0):
     max over ranks is the job's time.  Returns (max over ranks of the elapsed seconds, this rank's host
     submit time per step in ms: the time the host spends issuing one step's
     launches, which must stay well below the step's GPU time).  settle_ms:
-    untimed steps before the warmup (settle())."""
+    untimed steps before the warmup (settle()).  The steps issue their launches
+    only: no event between them (split_pass() times the launches right after);
+    two events bracket the region on the current stream, and `info`, if given,
+    receives their time per step ("gpu_ms_per_step")."""
     settle(step, settle_ms)
     for _ in range(warmup):
         step()
@@ -640,15 +709,43 @@ def timed(step, steps, warmup, world, settle_ms: float = 0.0):
     barrier(world)
     torch.cuda.synchronize()
     submit = 0.0
+    r0, r1 = Event(), Event()
     t0 = time.perf_counter()
+    r0.record()
     for _ in range(steps):
         s0 = time.perf_counter()
         step()
         submit += time.perf_counter() - s0
+    r1.record()
     torch.cuda.synchronize()
     own = time.perf_counter() - t0  # this rank's steps, up to its own synchronize
     barrier(world)
+    if info is not None:
+        info["gpu_ms_per_step"] = round(r0.elapsed_time(r1) / steps, 4)
     return max_over_ranks(own, world), submit / steps * 1e3
+
+
+def split_pass(launches, steps: int):
+    """Per-launch HIP-event durations for a step of several launches: `steps`
+    more steps right after the timed region, launches(i) being step i's launches
+    in issue order, with an event (Event, device-scope release) before the first
+    and after each, all on the current stream.  Returns (mean ms per launch
+    position, [per-step ms lists]).  Kept out of the timed region: every event
+    record holds the next launch back ~4 us whatever its release scope or form,
+    even bound to the dispatch by hipExtLaunchKernel (tools/tune/event_probe.hip,
+    profiles/r04/event_cost.txt), 2-3 % of a 0.44 ms headline step at three a step."""
+    evs = []
+    for i in range(steps):
+        fns = launches(i)
+        e = [Event() for _ in range(len(fns) + 1)]
+        e[0].record()
+        for j, f in enumerate(fns):
+            f()
+            e[j + 1].record()
+        evs.append(e)
+    torch.cuda.synchronize()
+    per = [[e[j].elapsed_time(e[j + 1]) for e in evs] for j in range(len(evs[0]) - 1)]
+    return [sum(x) / steps for x in per], per
 
 
 def graph_steps(fns):
@@ -742,14 +839,16 @@ def config_mixed(args, world, rank, dev):
                 cur.wait_event(done)
 
     run = graph_steps([step])[0] if args.graph else step
-    dt, submit = timed(run, args.steps, args.warmup, world, args.settle_ms)
+    info = {}  # the region's events sit on the current stream: one-stream runs only
+    dt, submit = timed(run, args.steps, args.warmup, world, args.settle_ms,
+                       info if lanes == 1 and len(streams) == 1 else None)
     ok = all(torch.equal(out[:, 0], st[:, 0]) for cl in copies for _, st, out in cl)
     data = 2 * 3 * (1 << 30)  # enc + dec, 3 classes, all ranks together
     per_class = {}  # outside the timed region: each class's kernels by HIP events (median of 9)
     for L, st, out in classes:
         t = {"encode": [], "decode": []}
         for _ in range(9):
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ev = [Event() for _ in range(3)]
             ev[0].record()
             encode_batch(coder, st[:, :k], st[:, k:])
             ev[1].record()
@@ -767,13 +866,13 @@ def config_mixed(args, world, rank, dev):
         return {"metric": f"GiB/s device-resident RS(6,4) encode+decode, mixed chunks: one GPU's share of an "
                           f"{parts}-GPU strong-scaled run", "value": round(per_gpu, 2), "unit": "GiB/s (this GPU)",
                 "n_gpus": world, "share_of": parts, "aggregate_if_ranks_scale": round(parts * per_gpu, 2),
-                "steps": args.steps, "ms_per_step": round(dt / args.steps * 1e3, 4),
+                "steps": args.steps, "ms_per_step": round(dt / args.steps * 1e3, 4), **info,
                 "host_submit_ms_per_step": round(submit, 4), "graph": bool(args.graph),
                 "streams": len(streams), "grouped": bool(args.mixed_group), "verified": ok, "classes": per_class, "data": "synthetic", "dtype": "u8", "higher_is_better": True,
                 "config": {"workload": f"rank 0's byte-balanced share of 1 GiB per class split {parts} ways"}}
     return {"metric": "GiB/s device-resident RS(6,4) encode+decode, mixed 1 KiB/4 KiB/1 MiB chunks",
             "value": round(args.steps * data / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), **info,
             "host_submit_ms_per_step": round(submit, 4), "graph": bool(args.graph), "streams": len(streams),
             "grouped": bool(args.mixed_group), "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic", "verified": ok, "classes": per_class,
@@ -795,17 +894,12 @@ def config_rs12(args, world, rank, dev):
     encode_batch(coder, st[:, :k], st[:, k:])
     out = torch.empty((Bc, e, Lc), dtype=torch.uint8, device=dev)
     surv = list(range(e, e + k))
-    evs = []
-
     def step():
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
         decode_batch(coder, st, surv, list(range(e)), out, inputs_by_unit=True)
-        e1.record()
-        evs.append((e0, e1))
 
-    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms)
-    ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
+    info = {}
+    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms, info)
+    (ms,), (per_step,) = split_pass(lambda i: [step], args.steps)
     ok = torch.equal(out, st[:, :e])
     alg = B * (k + e) * L
     gbs = alg / (ms * 1e-3) / 1e9
@@ -813,7 +907,7 @@ def config_rs12(args, world, rank, dev):
     par = st[:, k:].clone()
     enc_ev = []
     for _ in range(max(5, args.steps)):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0, e1 = Event(), Event()
         e0.record()
         encode_batch(coder, st[:, :k], st[:, k:])
         e1.record()
@@ -836,7 +930,7 @@ def config_rs12(args, world, rank, dev):
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                          "kernel": f"gf_apply_x16u<8,{e}> (decode)", "algorithmic_bytes_per_launch": alg},
-            **({"per_step_ms": [round(a.elapsed_time(b), 4) for a, b in evs[-args.steps:]]} if args.per_step else {}),
+            **info, **({"per_step_ms": [round(x, 4) for x in per_step]} if args.per_step else {}),
             "config": {"workload": f"RS(12,8) decode erase {set(range(e))} from {surv}, {B} x {L} B stripes per GPU",
                        "layout": LAYOUT_NAMES[layout_for(args, L)],
                        "parallelism": f"stripe-partitioned x{world}"}}
@@ -1050,17 +1144,12 @@ def config_update(args, world, rank, dev):
     old = torch.randint(0, 256, (B, L), dtype=torch.uint8, device=dev)
     new = torch.randint(0, 256, (B, L), dtype=torch.uint8, device=dev)
     par = torch.randint(0, 256, (B, m, L), dtype=torch.uint8, device=dev)
-    evs = []
-
     def step():
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
         encode_update_batch(coder, 1, old, new, par, par)
-        e1.record()
-        evs.append((e0, e1))
 
-    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms)
-    ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
+    info = {}
+    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms, info)
+    (ms,), _ = split_pass(lambda i: [step], args.steps)
     # self-check through the product: updating twice with the same delta restores the parity
     ref = par.clone()
     encode_update_batch(coder, 1, old, new, par, par)
@@ -1071,7 +1160,7 @@ def config_update(args, world, rank, dev):
     return {"metric": "GiB/s device-resident RS(6,4) parity update (encodeUpdate), 64 KiB chunks",
             "value": round(world * args.steps * B * L / dt / GIB, 2), "unit": "GiB/s (updated data bytes)",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(dt / args.steps * 1e3, 4), **info, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
@@ -1093,17 +1182,12 @@ def config_padded(args, world, rank, dev):
     else:
         lens = torch.full((B, k), int(float(args.pad_fill) * L), dtype=torch.int32, device=dev)
     par = torch.empty((B, m, L), dtype=torch.uint8, device=dev)
-    evs = []
-
     def step():
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
         encode_batch_padded(coder, data, lens, par)
-        e1.record()
-        evs.append((e0, e1))
 
-    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms)
-    ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
+    info = {}
+    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms, info)
+    (ms,), _ = split_pass(lambda i: [step], args.steps)
     # self-check through the product: explicit zero fill + plain encode gives the same parity
     idx = torch.arange(L, device=dev).view(1, 1, L)
     filled = torch.where(idx < lens.view(B, k, 1), data, torch.zeros((), dtype=torch.uint8, device=dev))
@@ -1116,7 +1200,7 @@ def config_padded(args, world, rank, dev):
     return {"metric": "GiB/s device-resident RS(6,4) zero-padded encode, 64 KiB codeLength",
             "value": round(world * args.steps * B * k * L / dt / GIB, 2), "unit": "GiB/s (codeLength bytes)",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(dt / args.steps * 1e3, 4), **info, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
@@ -1138,17 +1222,12 @@ def config_hashed(args, world, rank, dev):
     data = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev)
     par = torch.empty((B, m, L), dtype=torch.uint8, device=dev)
     hashes = torch.empty((B, m), dtype=torch.int32, device=dev)
-    evs = []
-
     def step():
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
         encode_batch_hashed(coder, data, par, hashes)
-        e1.record()
-        evs.append((e0, e1))
 
-    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms)
-    ms = sum(a.elapsed_time(b) for a, b in evs[-args.steps:]) / args.steps
+    info = {}
+    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms, info)
+    (ms,), _ = split_pass(lambda i: [step], args.steps)
     ref = torch.empty_like(par)
     encode_batch(coder, data, ref)
     # spot-check two hashes against the closed form on the host
@@ -1160,7 +1239,7 @@ def config_hashed(args, world, rank, dev):
     gbs = alg / (ms * 1e-3) / 1e9
     return {"metric": f"GiB/s device-resident RS(6,4) encode + fused parity hashCode, {L} B chunks",
             "value": round(world * args.steps * B * k * L / dt / GIB, 2), "unit": "GiB/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), **info,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic", "verified": ok,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -1260,22 +1339,14 @@ def config_flows(args, world, rank, dev):
 
         def dec_step():
             decode_batch_ex(coder, stripe, surv, [t], rebuilt, lengths=dlens, inputs_by_unit=True)
-    ev = {"encode": [], "update": [], "decode": []}
-
     def step():
-        es = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-        es[0].record()
         enc_step()
-        es[1].record()
         upd_step()
-        es[2].record()
         dec_step()
-        es[3].record()
-        for i, nm in enumerate(("encode", "update", "decode")):
-            ev[nm].append((es[i], es[i + 1]))
 
-    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms)
-    ms = {nm: sum(a.elapsed_time(b) for a, b in v[-args.steps:]) / args.steps for nm, v in ev.items()}
+    info = {}
+    dt, submit = timed(step, args.steps, args.warmup, world, args.settle_ms, info)
+    ms = dict(zip(("encode", "update", "decode"), split_pass(lambda i: [enc_step, upd_step, dec_step], args.steps)[0]))
     # self-check through the product (coded untiled, contiguous): the new parity is the
     # encode of the zero-filled stripe with unit t replaced, its hashes match, and the
     # degraded read returns the unit t its parity holds, zero filled
@@ -1301,7 +1372,7 @@ def config_flows(args, world, rank, dev):
     # same buffers (tiled: every tile whole), HIP events, median of 9 launches
     pe = []
     for _ in range(9):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0, e1 = Event(), Event()
         e0.record()
         encode_batch(coder, data, par)
         e1.record()
@@ -1320,7 +1391,7 @@ def config_flows(args, world, rank, dev):
             "value": round(world * args.steps * B * (2 * k + 1) * L / dt / GIB, 2),
             "unit": "GiB/s (codeLength bytes: k units encoded + 1 updated + k survivors decoded per stripe)",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4), "host_submit_ms_per_step": round(submit, 4),
+            "ms_per_step": round(dt / args.steps * 1e3, 4), **info, "host_submit_ms_per_step": round(submit, 4),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok, "kernels": kern,
             "plain_encode_same_layout": {"ms": round(plain_ms, 4),
@@ -1394,7 +1465,9 @@ def finish(out, rank, world, rec) -> None:
 
 
 def main():
+    global event_release
     args = parse()
+    event_release = args.event_release
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         # no launcher: start one rank per GPU (before anything touches the GPU here)
@@ -1460,57 +1533,46 @@ def main():
     if lanes is not None and (replays is not None or len(sets) % args.streams):
         raise SystemExit("--streams S needs eager launches and --rotate a multiple of S")
 
-    def step(ev=None):
+    def step():
         i = turn[0] % len(sets)
-        if lanes is not None and ev is None:  # batch i always on lane i % S: reuse stays ordered
-            turn[0] += 1
+        turn[0] += 1
+        if lanes is not None:  # batch i always on lane i % S: reuse stays ordered
             with torch.cuda.stream(lanes[i % len(lanes)]):
                 ops[i][0]()
                 ops[i][1]()
-            return
-        turn[0] += 1
-        if ev is not None:
-            ev[0].record(stream)
-        if replays is not None:  # one graph per batch: encode + decode
+        elif replays is not None:  # one graph per batch: encode + decode
             replays[i]()
         else:
             ops[i][0]()
-            if ev is not None:
-                ev[1].record(stream)
             ops[i][1]()
-        if ev is not None:
-            ev[2].record(stream)
 
     settle_steps = settle(step, args.settle_ms)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     barrier(world)
     torch.cuda.synchronize()
     submit = 0.0
+    r0, r1 = Event(), Event()  # the region on the GPU's clock (one-stream runs)
     t0 = time.perf_counter()
+    r0.record(stream)
     for i in range(args.steps):
         s0 = time.perf_counter()
-        step(evs[i] if lanes is None else None)
+        step()
         submit += time.perf_counter() - s0
+    r1.record(stream)
     torch.cuda.synchronize()
     own = time.perf_counter() - t0  # clock stops at this rank's synchronize; the
     barrier(world)                  # closing barrier's own latency is not a step's
     elapsed = max_over_ranks(own, world)
     submit_ms = submit / args.steps * 1e3
+    gpu_ms = r0.elapsed_time(r1) / args.steps if lanes is None else None
 
-    if replays is not None or lanes is not None:  # per-kernel split from an eager one-stream pass
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-        replays, keep = None, replays
-        for i in range(args.steps):
-            step(evs[i])
-        torch.cuda.synchronize()
-        replays = keep
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
-    dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    per_step = {"encode": [round(e[0].elapsed_time(e[1]), 4) for e in evs],
-                "decode": [round(e[1].elapsed_time(e[2]), 4) for e in evs]} if args.per_step else None
+    # per-kernel split: the next args.steps steps again, eager on one stream, an event around
+    # each launch (split_pass: events inside the timed region would cost it ~4 us a record)
+    (enc_ms, dec_ms), (enc_each, dec_each) = split_pass(lambda i: list(ops[(turn[0] + i) % len(sets)]), args.steps)
+    per_step = {"encode": [round(x, 4) for x in enc_each],
+                "decode": [round(x, 4) for x in dec_each]} if args.per_step else None
     if args.decode_out == "inplace":  # unit 0 was rebuilt in place: it must still be the original data
         ok = bool(torch.equal(stripe[:, 0], orig0))
     else:
@@ -1550,6 +1612,8 @@ def main():
             "settle": {"ms": args.settle_ms, "steps": settle_steps},  # untimed, before the warmup steps
         },
         "host_submit_ms_per_step": round(submit_ms, 4),
+        # the timed region on the GPU's clock: two events around it on the launch stream
+        "gpu_ms_per_step": round(gpu_ms, 4) if gpu_ms is not None else None,
         "roofline": {
             "bound": "hbm",
             "achieved": round(enc_gbs, 1),
@@ -1560,6 +1624,8 @@ def main():
             "kernel": "gf_apply_x16u<4,2> (encode)",
             "algorithmic_bytes_per_launch": enc_alg,
             "traffic_source": traffic_src,
+            "timing": f"HIP events (device-scope release) around each launch of {args.steps} steps run right "
+                      "after the timed region, same launches and stream (split_pass)",
         },
         "kernels": {
             "encode": {"ms": round(enc_ms, 4), "GB/s": round(enc_gbs, 1),
