@@ -84,9 +84,16 @@ hipError_t scratch_lease(hipStream_t stream, size_t words, ScratchEntry** out)
             e->ptr = nullptr;
             e->words = 0;
             if (err == hipSuccess) err = hipMalloc(reinterpret_cast<void**>(&e->ptr), words * sizeof(uint32_t));
+            // zero once: the first half's accumulators are zero at rest (hash_scratch_need)
+            if (err == hipSuccess) err = hipMemsetAsync(e->ptr, 0, words * sizeof(uint32_t), stream);
             if (err == hipSuccess) e->words = words;
         }
-        if (err == hipSuccess && !e->done) err = hipEventCreateWithFlags(&e->done, hipEventDisableTiming);
+        // A completion marker only the host waits on: no timestamp, and a device-scope
+        // release (nothing on the host reads the partials).  The default system-scope
+        // record cost the stream ~3 us per hashed call against ~1.5 us this way
+        // (tools/tune/event_probe.hip, profiles/r04/event_cost.txt).
+        if (err == hipSuccess && !e->done)
+            err = hipEventCreateWithFlags(&e->done, hipEventDisableTiming | hipEventDisableSystemFence);
         if (err != hipSuccess) {
             e->mu.unlock();
             return err;

@@ -239,6 +239,8 @@ for step in "$@"; do
             args="--config rs12 --steps 20 --warmup 3"
             [ $cfg = headline ] && args="--no-cpu --no-host --no-sizes --no-configs --steps 20 --warmup 3"
             [ $cfg = hashed ] && args="--config hashed --steps 20 --warmup 3"
+            [ $cfg = flows ] && args="--config flows --steps 20 --warmup 3"
+            [ $cfg = update ] && args="--config update --steps 20 --warmup 3"
             for pass in A B C; do
                 ctr=$PA; [ $pass = B ] && ctr=$PB; [ $pass = C ] && ctr=$PC
                 [ -n "$ctr" ] || continue

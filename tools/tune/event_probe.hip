@@ -45,10 +45,11 @@ int main(int argc, char** argv)
     CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     const dim3 grid(unsigned(n / 256)), block(256);
     const char* names[] = {"plain", "record default", "record device-scope", "ext-launch default",
-                           "ext-launch device-scope"};
+                           "ext-launch device-scope", "1 record no-timing", "1 record no-timing dev"};
     for (int round = 0; round < 2; ++round) {
-        for (int mode = 0; mode < 5; ++mode) {
-            const unsigned flags = (mode == 2 || mode == 4) ? hipEventDisableSystemFence : 0;
+        for (int mode = 0; mode < 7; ++mode) {
+            unsigned flags = (mode == 2 || mode == 4 || mode == 6) ? hipEventDisableSystemFence : 0;
+            if (mode >= 5) flags |= hipEventDisableTiming;  // a completion marker only (the scratch lease's)
             std::vector<hipEvent_t> ev(2 * reps);
             for (auto& e : ev) CHECK(hipEventCreateWithFlags(&e, flags));
             for (int w = 0; w < 4; ++w) hipLaunchKernelGGL(copy_kernel, grid, block, 0, s, src, dst, n);
@@ -57,6 +58,9 @@ int main(int argc, char** argv)
             for (int i = 0; i < reps; ++i) {
                 if (mode == 0) {
                     hipLaunchKernelGGL(copy_kernel, grid, block, 0, s, src, dst, n);
+                } else if (mode >= 5) {
+                    hipLaunchKernelGGL(copy_kernel, grid, block, 0, s, src, dst, n);
+                    CHECK(hipEventRecord(ev[2 * i], s));
                 } else if (mode <= 2) {
                     CHECK(hipEventRecord(ev[2 * i], s));
                     hipLaunchKernelGGL(copy_kernel, grid, block, 0, s, src, dst, n);
@@ -68,14 +72,14 @@ int main(int argc, char** argv)
             CHECK(hipStreamSynchronize(s));
             double wall = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
             double sum = 0;
-            if (mode > 0)
+            if (mode > 0 && mode < 5)
                 for (int i = 0; i < reps; ++i) {
                     float ms = 0;
                     CHECK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
                     sum += ms * 1e3;
                 }
             std::printf("round %d  %-24s wall %8.2f us/kernel  event-timed %8.2f us/kernel\n", round, names[mode],
-                        wall / reps, mode ? sum / reps : 0.0);
+                        wall / reps, (mode > 0 && mode < 5) ? sum / reps : 0.0);
             for (auto& e : ev) CHECK(hipEventDestroy(e));
         }
     }
