@@ -430,11 +430,8 @@ private:
                 if (e != hipSuccess) return map_hip(e);
             }
             hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_hash_), kern::kMaxRows * sizeof(int32_t));
-            for (int s = 0; s < kSlots && e == hipSuccess; ++s) {
+            for (int s = 0; s < kSlots && e == hipSuccess; ++s)
                 e = hipMalloc(reinterpret_cast<void**>(&d_scratch_[s]), kScratchWords * sizeof(uint32_t));
-                if (e == hipSuccess)  // zero once: the accumulators are zero at rest (kern::hash_scratch_need)
-                    e = hipMemset(d_scratch_[s], 0, kScratchWords * sizeof(uint32_t));
-            }
             if (e != hipSuccess) return map_hip(e);
         }
         if (in_bytes > cap_in_) {
@@ -837,8 +834,6 @@ private:
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_hash), meta);
             s.scratch_words = kern::hash_scratch_need(arena / 16);  // a batch has at most arena/16 segments
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_scratch), s.scratch_words * sizeof(uint32_t));
-            if (e == hipSuccess)  // zero once: the accumulators are zero at rest (kern::hash_scratch_need)
-                e = hipMemset(s.d_scratch, 0, s.scratch_words * sizeof(uint32_t));
             if (e != hipSuccess) return map_hip(e);
             s.dsrc.reset(new (std::nothrow) const uint8_t*[kMaxDirectSlots * kern::kMaxCols]);
             s.dsrc_n.reset(new (std::nothrow) size_t[kMaxDirectSlots * kern::kMaxCols]);

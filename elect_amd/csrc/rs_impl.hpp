@@ -145,12 +145,7 @@ struct LaunchPolicy {
     int plain_lds_dma = 1;
     // The parity hash's per-wave sum weights each lane by 31^(16 lane) inside a DPP tree
     // (wave_poly31) instead of a per-lane table load that waits behind the parity stores.
-    // Neutral on hashed, -1 point on the padded whole-wave steps (profiles/r04/hash_dpp_ab.txt).
     bool hash_dpp_weights = false;
-    // Assign-mode hashes of launches whose waves all lie inside one hashed unit: each wave
-    // adds its partial and one arrival into its unit's 64-bit accumulator, and the unit's
-    // last arrival writes the hash (hash_finalize), so no hash_reduce launch follows.
-    bool hash_fused_finalize = false;
 };
 
 #ifdef ELECT_EC_POLICY_HEADER
@@ -438,29 +433,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 // to 8 dwords so one ds_read_b128 + one ds_read_b32 (wave-uniform address,
 // broadcast) bring a coefficient's tables into VGPRs; keeping 32 coefficients
 // (RS(12,8)) in SGPRs instead spills.
-// Fused finalize of a whole wave's parity-hash partials (kPolicy.hash_fused_finalize).
-// Lane 0 adds the wave's partial and one arrival into its unit's accumulator (the
-// arrival count in bits 63:48, the sum in 47:0: at most 65,535 waves of < 2^32
-// each, so no carry reaches the count), one 64-bit device-scope atomic per row.
-// The partial travels inside the atomic, so no fence orders it against the
-// count.  The unit's last arrival writes 31^len + sum (mod 2^32) and returns the
-// accumulator to zero for the next launch.
-template <int R>
-__device__ __forceinline__ void hash_finalize(const uint32_t (&sum)[R], unsigned long long* acc, uint32_t waves,
-                                              int32_t* h, uint32_t seed)
-{
-    if ((threadIdx.x & 63u) != 0) return;
-    unsigned long long old[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) old[r] = atomicAdd(acc + r, (1ull << 48) + sum[r]);
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-        if ((old[r] >> 48) == waves - 1u) {
-            h[r] = static_cast<int32_t>(seed + static_cast<uint32_t>(old[r] + sum[r]));
-            atomicExch(acc + r, 0ull);
-        }
-}
-
 // ---------------------------------------------------------------------------
 template <int K, int R>
 struct FastArgs {
@@ -490,9 +462,6 @@ struct FastArgs {
     uint32_t hpow;          // 31^(hash offset of byte 0 of this launch window)
     uint32_t* hpart;        // per-wave partial sums [wave][R]: the wave's first stripe
     uint32_t* hpart_hi;     // assign mode: [wave][R] sums of a straddling wave's second stripe, else null
-    unsigned long long* hacc;  // fused finalize: [unit][R] accumulators, zero at rest, else null
-    uint32_t hwaves;        // fused finalize: waves per hashed unit (hsegs / 64, < 2^16)
-    uint32_t hseed;         // fused finalize: 31^(unit length), the hash of the empty prefix
     gf::PermTable tab[R][K];
 };
 
@@ -747,20 +716,14 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16(const FastArgs<K, R> a)
         if (whole_wave) {  // partial sums to scratch; hash_reduce adds them per stripe
             const uint32_t seg0 = first - s_first * a.hsegs;
             const uint32_t p0 = a.hpow * pow31_seg(seg0);
-            uint32_t sum[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
+                uint32_t sum;
                 if constexpr (kPolicy.hash_dpp_weights)
-                    sum[r] = p0 * wave_poly31(horner31(acc[r]));
+                    sum = p0 * wave_poly31(horner31(acc[r]));
                 else
-                    sum[r] = wave_sum(horner31(acc[r]) * (kLanePow.v[threadIdx.x & 63u] * p0));
-            }
-            if (kPolicy.hash_fused_finalize && a.hacc) {
-                hash_finalize<R>(sum, a.hacc + static_cast<uint64_t>(s_first) * R, a.hwaves,
-                                 a.hashes + static_cast<uint64_t>(s_first) * a.hstride, a.hseed);
-            } else if ((threadIdx.x & 63u) == 0) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum[r];
+                    sum = wave_sum(horner31(acc[r]) * (kLanePow.v[threadIdx.x & 63u] * p0));
+                if ((threadIdx.x & 63u) == 0) a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum;
             }
         } else if (a.hpart_hi) {  // assign mode: a wave straddling two stripes (or the launch's end)
             const uint32_t p = live ? a.hpow * pow31_seg(hseg) : 0u;
@@ -821,20 +784,14 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16u(const FastArgs<K, R> a)
         if (a.hashes) {
             const uint32_t hs = div_magic(first, a.hmagic, a.hshift);
             const uint32_t p0 = a.hpow * pow31_seg(first - hs * a.hsegs);
-            uint32_t sum[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
+                uint32_t sum;
                 if constexpr (kPolicy.hash_dpp_weights)
-                    sum[r] = p0 * wave_poly31(horner31(acc[r]));
+                    sum = p0 * wave_poly31(horner31(acc[r]));
                 else
-                    sum[r] = wave_sum(horner31(acc[r]) * (kLanePow.v[threadIdx.x & 63u] * p0));
-            }
-            if (kPolicy.hash_fused_finalize && a.hacc) {
-                hash_finalize<R>(sum, a.hacc + static_cast<uint64_t>(hs) * R, a.hwaves,
-                                 a.hashes + static_cast<uint64_t>(hs) * a.hstride, a.hseed);
-            } else if ((threadIdx.x & 63u) == 0) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum[r];
+                    sum = wave_sum(horner31(acc[r]) * (kLanePow.v[threadIdx.x & 63u] * p0));
+                if ((threadIdx.x & 63u) == 0) a.hpart[static_cast<uint64_t>(first >> 6) * R + r] = sum;
             }
         }
     }
@@ -1146,11 +1103,6 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
     for (int r = 0; r < R; ++r)
         for (int j = 0; j < K; ++j) a.tab[r][j] = gf::perm_table(p.coef[(r0 + r) * p.cols + j]);
     const bool hash_assign = p.hashes && p.hash_seed;  // launch_apply chose assign mode
-    // Fused finalize: assign mode with every wave inside one hashed unit (units of whole
-    // waves, so launches of whole units hold whole waves too) and a count that fits
-    // the accumulator's 16 bits.  (The accumulators take (total / 64 + 1) * R of the
-    // scratch's first half, as the partials do of its second.)
-    const bool fused_hash = hash_assign && a.hsegs % 64 == 0 && a.hsegs / 64 < (1u << 16);
     // scalar stripe bases: plain launches of whole-wave stripes (kPolicy.scalar_base_min_cols
     // columns and up; hashed ones of any width)
     const bool whole_waves = !PAD && a.segs % 64 == 0 && segs64 < (uint64_t{1} << 28);
@@ -1173,18 +1125,11 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
         a.total = static_cast<uint32_t>(ns * segs64);
         a.hpart = nullptr;
         a.hpart_hi = nullptr;
-        a.hacc = nullptr;
-        if (a.hashes) {  // scratch: [unit][row] accumulators (zero at rest), then the per-wave partials
+        if (a.hashes) {  // the per-wave partial sums (lo, then hi) go to the caller's scratch
             const size_t n = (static_cast<size_t>(a.total) / 64 + 1) * R;
-            const size_t half = p.hash_scratch_words / 2;
-            if (!p.hash_scratch || 2 * n > half) return hipErrorInvalidValue;
-            a.hpart = p.hash_scratch + half;
+            if (!p.hash_scratch || 2 * n > p.hash_scratch_words) return hipErrorInvalidValue;
+            a.hpart = p.hash_scratch;
             if (hash_assign) a.hpart_hi = a.hpart + n;
-            if (kPolicy.hash_fused_finalize && fused_hash) {
-                a.hacc = reinterpret_cast<unsigned long long*>(p.hash_scratch);
-                a.hwaves = a.hsegs / 64;
-                a.hseed = pow31(ulen);
-            }
         }
         constexpr int kCoefs = R * K;
         if constexpr (PAD) {
@@ -1234,7 +1179,7 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             }  // (launch_apply rejects hashed launches wider than kMaxHashCols)
         }
         hipError_t e = hipGetLastError();
-        if (e == hipSuccess && a.hashes && !a.hacc) {
+        if (e == hipSuccess && a.hashes) {
             const uint32_t units = static_cast<uint32_t>(ns / tiles);
             const uint32_t n = units * R;  // one wave each
             hipLaunchKernelGGL(hash_reduce, dim3((n + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, stream, a.hpart,

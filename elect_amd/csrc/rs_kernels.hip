@@ -84,8 +84,6 @@ hipError_t scratch_lease(hipStream_t stream, size_t words, ScratchEntry** out)
             e->ptr = nullptr;
             e->words = 0;
             if (err == hipSuccess) err = hipMalloc(reinterpret_cast<void**>(&e->ptr), words * sizeof(uint32_t));
-            // zero once: the first half's accumulators are zero at rest (hash_scratch_need)
-            if (err == hipSuccess) err = hipMemsetAsync(e->ptr, 0, words * sizeof(uint32_t), stream);
             if (err == hipSuccess) e->words = words;
         }
         // A completion marker only the host waits on: no timestamp, and a device-scope

@@ -121,10 +121,7 @@ hipError_t launch_apply_many(const ApplyParams* ps, int n, hipStream_t stream);
 
 // Scratch words a hashed launch_apply over `segments` 16-byte segments in all
 // (stripes x ceil(len/16)) needs at most (row groups run one after another).
-// Its first half holds 64-bit per-(unit, row) accumulators that must be zero
-// when the buffer is first used (every launch that uses them leaves them zero):
-// zero a new scratch buffer once.  The second half holds per-wave partials.
-constexpr size_t hash_scratch_need(uint64_t segments) { return 2 * (segments / 64 + 1) * kFastRows * 2; }
+constexpr size_t hash_scratch_need(uint64_t segments) { return (segments / 64 + 1) * kFastRows * 2; }
 hipError_t launch_update(const UpdateParams& p, hipStream_t stream);
 
 // True when every column start is 16-byte aligned for every stripe.
