@@ -120,6 +120,8 @@ def parse():
                     help="HBM layout of the stripes ([B][k+m][L] or [k+m][B][L]); headline and mixed. auto: "
                          "unit-major for chunks <= 4 KiB (a stripe-major wave would read and write one "
                          "6 KiB region), stripe-major above")
+    ap.add_argument("--column-skew", type=int, default=0,
+                    help="unit-major layout experiment: bytes of gap between one column's region and the next's")
     ap.add_argument("--decode-out", choices=("separate", "inplace"), default="separate",
                     help="headline decode target: a separate [B][1][L] buffer, or the erased unit's own slot")
     ap.add_argument("--rotate", type=int, default=4,
@@ -668,7 +670,12 @@ def alloc_stripes(args, B: int, L: int, k: int, m: int, dev, generator=None):
         st = torch.empty((B, t, k + m, TILE), dtype=torch.uint8, device=dev).view(B * t, k + m, TILE)
         Bc, Lc = B * t, TILE
     elif layout == "unit":
-        st = torch.empty((k + m, B, L), dtype=torch.uint8, device=dev).transpose(0, 1)
+        skew = getattr(args, "column_skew", 0)  # bytes between one column's end and the next's start
+        if skew:
+            base = torch.empty((k + m) * (B * L + skew), dtype=torch.uint8, device=dev)
+            st = base.as_strided((B, k + m, L), (L, B * L + skew, 1))
+        else:
+            st = torch.empty((k + m, B, L), dtype=torch.uint8, device=dev).transpose(0, 1)
         Bc, Lc = B, L
     else:
         st = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
