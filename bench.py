@@ -1466,6 +1466,8 @@ def finish(out, rank, world, rec) -> None:
     out["build"] = {"id": _lib.BUILD_ID, "from_these_sources": _lib.BUILD_CURRENT}
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if not rec["verified"]:  # say which check failed (the line's records hold the flags)
+        print(f"bench.py: rank {rank} failed verification: {json.dumps(rec)}", file=sys.stderr, flush=True)
     dist.teardown(world)
     if not ok:
         sys.exit(1)
