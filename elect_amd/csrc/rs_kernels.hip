@@ -12,8 +12,12 @@ namespace kern {
 namespace {
 
 // Hash-partial scratch when the caller brings none (the device-resident API):
-// one buffer per (device, stream), reused only in that stream's order, grown or
-// handed to another stream only after an event recorded behind its last use.
+// one buffer per (device, stream), reused only in that stream's order.  It is
+// handed to another stream (16 entries per device, least recently used first)
+// only after a device-wide synchronize, and grown only after its own stream's
+// synchronize, so a hashed call records nothing on the stream: a completion
+// marker behind every call held the next launch back ~1.5 us (round 4,
+// profiles/r04/event_cost.txt), and streams beyond 16 are rare.
 // Stream-ordered allocation (hipMallocAsync / hipFreeAsync, default or private
 // pool) corrupted partials when many threads launched on their own streams:
 // freed blocks were handed out again while a reduce still read them
@@ -25,9 +29,8 @@ struct ScratchEntry {
     uint64_t last = 0;       // LRU tick (under the cache mutex)
     uint32_t* ptr = nullptr;
     size_t words = 0;
-    hipEvent_t done = nullptr;  // recorded behind the last launch that used ptr
-    hipStream_t done_on = nullptr;
-    bool recorded = false;
+    hipStream_t owner = nullptr;  // the stream whose launches may still read ptr
+    bool owned = false;
 };
 
 struct ScratchCache {
@@ -38,7 +41,7 @@ struct ScratchCache {
 
 ScratchCache g_scratch[64];
 
-// Returns with entry->mu held; scratch_release() records the event and unlocks.
+// Returns with entry->mu held; scratch_release() unlocks.
 hipError_t scratch_lease(hipStream_t stream, size_t words, ScratchEntry** out)
 {
     // The scratch is allocated on, and cached for, the current device: a stream of
@@ -73,41 +76,32 @@ hipError_t scratch_lease(hipStream_t stream, size_t words, ScratchEntry** out)
             e->mu.unlock();
             continue;
         }
-        if (e->recorded && e->done_on != stream) {  // last used on another stream: wait for it
-            err = hipEventSynchronize(e->done);
-            e->recorded = err != hipSuccess;
-        }
+        // Last used on another stream (which may since have been destroyed): wait for
+        // the whole device, then this stream owns the buffer.
+        if (e->owned && e->owner != stream) err = hipDeviceSynchronize();
         if (err == hipSuccess && e->words < words) {
-            if (e->recorded) err = hipEventSynchronize(e->done);  // its last use on this stream
-            e->recorded = false;
+            if (e->owned) err = hipStreamSynchronize(stream);  // its last use, on this stream
             if (err == hipSuccess && e->ptr) err = hipFree(e->ptr);
             e->ptr = nullptr;
             e->words = 0;
             if (err == hipSuccess) err = hipMalloc(reinterpret_cast<void**>(&e->ptr), words * sizeof(uint32_t));
             if (err == hipSuccess) e->words = words;
         }
-        // A completion marker only the host waits on: no timestamp, and a device-scope
-        // release (nothing on the host reads the partials).  The default system-scope
-        // record cost the stream ~3 us per hashed call against ~1.5 us this way
-        // (tools/tune/event_probe.hip, profiles/r04/event_cost.txt).
-        if (err == hipSuccess && !e->done)
-            err = hipEventCreateWithFlags(&e->done, hipEventDisableTiming | hipEventDisableSystemFence);
         if (err != hipSuccess) {
             e->mu.unlock();
             return err;
         }
+        e->owner = stream;
+        e->owned = true;
         *out = e;
         return hipSuccess;
     }
 }
 
-hipError_t scratch_release(ScratchEntry* e, hipStream_t stream)
+hipError_t scratch_release(ScratchEntry* e, hipStream_t)
 {
-    const hipError_t err = hipEventRecord(e->done, stream);
-    e->recorded = err == hipSuccess;
-    e->done_on = stream;
     e->mu.unlock();
-    return err;
+    return hipSuccess;
 }
 
 // Every (cols, rows) launcher, by source-column count (rs_inst.hip).  Padded
