@@ -744,6 +744,18 @@ private:
         uint8_t coef[kern::kMaxRows * kern::kMaxCols] = {};
     };
 
+    // A direct batch's unit pointers, copied out of its slab under mu_ by the
+    // dispatcher (the callers write them before taking mu_ to count themselves
+    // filled).  issue() reads only this copy: the slab's arrays are rewritten for
+    // its next batch once this one completes, and the only order between that and
+    // issue()'s reads would otherwise run through the HIP stream (ThreadSanitizer,
+    // profiles/r04/tsan_summary.txt).
+    struct DirectSlots {
+        std::vector<const uint8_t*> src;
+        std::vector<size_t> src_n;
+        std::vector<uint8_t*> dst;
+    };
+
     struct Slab {
         enum State { kFree, kOpen, kInFlight, kDone } state = kFree;
         Batcher* owner = nullptr;
@@ -840,6 +852,13 @@ private:
             s.ddst.reset(new (std::nothrow) uint8_t*[kMaxDirectSlots * kern::kMaxRows]);
             if (!s.dsrc || !s.dsrc_n || !s.ddst) return ELECT_EC_ENOMEM;
         }
+        try {  // the dispatcher's copies never grow past this (no allocation on its thread)
+            slots_.src.reserve(kMaxDirectSlots * kern::kMaxCols);
+            slots_.src_n.reserve(kMaxDirectSlots * kern::kMaxCols);
+            slots_.dst.reserve(kMaxDirectSlots * kern::kMaxRows);
+        } catch (const std::bad_alloc&) {
+            return ELECT_EC_ENOMEM;
+        }
         return ELECT_EC_OK;
     }
 
@@ -898,8 +917,14 @@ private:
             cv_worker_.wait(lock, [&] { return s->filled == s->reserved; });
             const Shape shape = s->shape();  // under mu_: open() rewrites these for the slab's next batch
             const int n = s->reserved;
+            if (shape.direct) {
+                const size_t ni = static_cast<size_t>(n) * kern::kMaxCols, no = static_cast<size_t>(n) * kern::kMaxRows;
+                slots_.src.assign(s->dsrc.get(), s->dsrc.get() + ni);
+                slots_.src_n.assign(s->dsrc_n.get(), s->dsrc_n.get() + ni);
+                slots_.dst.assign(s->ddst.get(), s->ddst.get() + no);
+            }
             lock.unlock();
-            const hipError_t e = issue(*s, shape, n);
+            const hipError_t e = issue(*s, shape, n, slots_);
             if (e != hipSuccess) (void)hipStreamSynchronize(s->stream);  // no callback was queued
             lock.lock();
             if (e != hipSuccess) finish(s, map_hip(e));
@@ -909,7 +934,7 @@ private:
 
     // s's buffers, stream and event never change after init(); its shape is
     // read from the copy taken under mu_.
-    static hipError_t issue(Slab& s, const Shape& sh, int n)
+    static hipError_t issue(Slab& s, const Shape& sh, int n, const DirectSlots& d)
     {
         const size_t in_stride = sh.tiles * sh.cols * sh.pitch;  // per slot
         const size_t out_stride = sh.tiles * sh.rows * sh.pitch;
@@ -920,8 +945,8 @@ private:
             for (int q = 0; q < n && e == hipSuccess; ++q)
                 for (int j = 0; j < sh.cols && e == hipSuccess; ++j) {
                     const size_t i = static_cast<size_t>(q) * kern::kMaxCols + j;
-                    if (s.dsrc_n[i])
-                        e = hipMemcpyAsync(s.d_in + q * in_stride + j * sh.pitch, s.dsrc[i], s.dsrc_n[i],
+                    if (d.src_n[i])
+                        e = hipMemcpyAsync(s.d_in + q * in_stride + j * sh.pitch, d.src[i], d.src_n[i],
                                            hipMemcpyHostToDevice, s.stream);
                 }
         } else {
@@ -963,7 +988,7 @@ private:
         if (e == hipSuccess && sh.direct) {
             for (int q = 0; q < n && e == hipSuccess; ++q)
                 for (int r = 0; r < sh.rows && e == hipSuccess; ++r)
-                    e = hipMemcpyAsync(s.ddst[static_cast<size_t>(q) * kern::kMaxRows + r], s.d_out + q * out_stride + r * sh.pitch,
+                    e = hipMemcpyAsync(d.dst[static_cast<size_t>(q) * kern::kMaxRows + r], s.d_out + q * out_stride + r * sh.pitch,
                                        sh.len, hipMemcpyDeviceToHost, s.stream);
         } else if (e == hipSuccess) {
             e = hipMemcpyAsync(s.pin_out, s.d_out, n * out_stride, hipMemcpyDeviceToHost, s.stream);
@@ -1001,6 +1026,7 @@ private:
     // every reservation: O(callers^2) wake-ups per batch at 64 callers).
     std::mutex mu_;
     std::condition_variable cv_worker_;  // the dispatcher
+    DirectSlots slots_;                  // the dispatcher's copy of a direct batch's slots (its thread only)
     std::condition_variable cv_slot_;    // callers waiting for an arena to reserve in
     bool started_ = false;
     bool init_failed_ = false;  // the arenas could not be allocated: every call runs directly
