@@ -114,8 +114,16 @@ public:
             p = std::aligned_alloc(4096, cls);
             if (!p) return nullptr;
         }
-        std::unique_lock<std::shared_mutex> lock(mu_);
-        live_[reinterpret_cast<uintptr_t>(p)] = Block{cls, pinned};
+        try {
+            std::unique_lock<std::shared_mutex> lock(mu_);
+            live_[reinterpret_cast<uintptr_t>(p)] = Block{cls, pinned};
+        } catch (...) {  // no record, no buffer: nothing leaks
+            if (pinned)
+                (void)hipHostFree(p);
+            else
+                std::free(p);
+            return nullptr;
+        }
         return p;
     }
 
@@ -129,9 +137,12 @@ public:
             b = it->second;
             live_.erase(it);
             if (b.pinned && free_bytes_ + b.size <= cap()) {
-                free_[b.size].push_back(p);
-                free_bytes_ += b.size;
-                return true;
+                try {
+                    free_[b.size].push_back(p);
+                    free_bytes_ += b.size;
+                    return true;
+                } catch (...) {  // no room in the free list: release the buffer below
+                }
             }
         }
         if (b.pinned)
