@@ -28,7 +28,7 @@ def _bench():
 def _workload(dev):
     from elect_amd.batch import decode_batch, encode_batch
     from elect_amd.coder import RSCoder
-    k, m, L, B = 4, 2, 65536, 512
+    k, m, L, B = 4, 2, 65536, 2048  # a step of ~0.2 ms: the events' few us are small beside it
     coder = RSCoder(k, m)
     st = torch.empty((B, k + m, L), dtype=torch.uint8, device=dev)
     st[:, :k] = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev)
@@ -73,7 +73,7 @@ def test_timed_and_split_pass(dev):
     means, per = bench.split_pass(lambda i: [enc, dec], steps)
     assert len(means) == 2 and len(per) == 2 and all(len(x) == steps for x in per)
     assert all(x > 0 for x in means)
-    # the launches' own times add up to the event-free step, up to the launch gaps
-    # and the few microseconds each event record adds around them
-    assert 0.85 * gpu_ms <= sum(means) <= 1.10 * gpu_ms, (means, gpu_ms)
+    # the launches' own times add up to the event-free step, up to the launch gaps and
+    # the few microseconds each event record adds around a launch (~4 us, two launches)
+    assert 0.85 * gpu_ms <= sum(means) <= 1.05 * gpu_ms + 0.012, (means, gpu_ms)
     assert torch.equal(out[:, 0], st[:, 0])  # the launches coded: erase-0 decode restores unit 0
