@@ -589,16 +589,24 @@ def device_copy_rate(dev, nbytes=1 << 30, reps=5):
     return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
 
 
-PROBE_SHAPES = ((256, 0), (64, 18))  # (block, waves per CU): tools/tune/tune_apply's probe; the plain coding launches
+# (block, waves per CU, XCD-major order): tools/tune/tune_apply's probe; the plain coding launches;
+# and the read shape tools/tune/ceiling_probe.hip found fastest (2 GiB at 7.57-7.62 TB/s on two
+# boxes, against 6.87-7.06 in dispatch order: each XCD streaming one contiguous eighth)
+PROBE_SHAPES = ((256, 0, False), (64, 18, False), (256, 24, True))
+# the coding kernels' own stream mixes (4 in, 1 or 2 out): the one-wave shapes they launch, and
+# the XCD-major shape that helps 256-thread blocks (profiles/r04/ceiling_probe.txt)
+MIX_SHAPES = ((64, 0, False), (64, 18, False), (256, 18, True))
 
 
 def hbm_ceilings(dev, nbytes=1 << 31, reps=9):
     """The HBM ceilings the coding kernels are judged against, measured on this GPU
     by the library's own probe kernels (elect_ec_hbm_probe: 16 bytes per lane, the
-    coding kernels' non-temporal loads and stores) over 2 GiB buffers: read, write
-    and copy (read + write bytes counted), each the best of two launch shapes
-    (PROBE_SHAPES) by the median of `reps` launches timed with HIP events on the
-    stream they run on.  The achievable figures beside the 8 TB/s spec peak."""
+    coding kernels' non-temporal loads and stores): read, write and copy over 2 GiB
+    buffers (read + write bytes counted), each the best of PROBE_SHAPES, and the
+    decode- and encode-shaped mixes (four 512 MiB streams XORed into one or two),
+    each the best of MIX_SHAPES; every figure the median of `reps` launches timed
+    with HIP events on the stream they run on.  The achievable figures beside the
+    8 TB/s spec peak."""
     from elect_amd import _lib
     # bytes below 0x80: the read probe's sink condition (a segment whose four dwords XOR to
     # 0x9E3779B9, rs_kernels.hip hbm_probe_kernel) can then never hold.  Over uniform random
@@ -608,14 +616,17 @@ def hbm_ceilings(dev, nbytes=1 << 31, reps=9):
     b = torch.empty_like(a)
     sink = torch.zeros(256, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
-    kinds = {"read": (0, a, sink, 1), "write": (1, None, b, 1), "copy": (2, a, b, 2)}
+    quarter = nbytes // 4
+    kinds = {"read": (0, a, sink, nbytes, 1, PROBE_SHAPES), "write": (1, None, b, nbytes, 1, PROBE_SHAPES),
+             "copy": (2, a, b, nbytes, 2, PROBE_SHAPES),
+             "decode_shape": (3, a, b, quarter, 5, MIX_SHAPES), "encode_shape": (4, a, b, quarter, 6, MIX_SHAPES)}
     res = {}
-    for name, (kind, src, dst, mult) in kinds.items():
+    for name, (kind, src, dst, n, mult, shapes) in kinds.items():
         best = 0.0
-        for block, waves in PROBE_SHAPES:
+        for block, waves, xcd in shapes:
             def launch():
-                _lib.hbm_probe(kind, src.data_ptr() if src is not None else 0, dst.data_ptr(), nbytes, block, waves,
-                               stream.cuda_stream)
+                _lib.hbm_probe(kind | (0x100 if xcd else 0), src.data_ptr() if src is not None else 0, dst.data_ptr(),
+                               n, block, waves, stream.cuda_stream)
             launch()
             ts = []
             for _ in range(reps):
@@ -625,8 +636,8 @@ def hbm_ceilings(dev, nbytes=1 << 31, reps=9):
                 e1.record(stream)
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1))
-            gbs = mult * nbytes / (sorted(ts)[reps // 2] * 1e-3) / 1e9
-            res[f"{name}_{block}x{waves}"] = round(gbs, 1)
+            gbs = mult * n / (sorted(ts)[reps // 2] * 1e-3) / 1e9
+            res[f"{name}_{block}x{waves}{'_xcd' if xcd else ''}"] = round(gbs, 1)
             best = max(best, gbs)
         res[name] = round(best, 1)
     if bool(sink.any()):
@@ -1684,7 +1695,13 @@ def main():
         rf["frac_of_copy"] = round(enc_gbs / ceil["copy"], 4)
         rf["decode_frac_of_copy"] = round(dec_gbs / ceil["copy"], 4)
         rf["frac_of_read"] = round(enc_gbs / ceil["read"], 4)
-        rf["ceiling_probes"] = {key: v for key, v in ceil.items() if "_" in key}
+        # against probes with the kernels' own stream mix (4 in, 2 out / 4 in, 1 out)
+        rf["device_encode_shape_GB/s"] = ceil["encode_shape"]
+        rf["device_decode_shape_GB/s"] = ceil["decode_shape"]
+        rf["frac_of_encode_shape"] = round(enc_gbs / ceil["encode_shape"], 4)
+        rf["decode_frac_of_decode_shape"] = round(dec_gbs / ceil["decode_shape"], 4)
+        rf["ceiling_probes"] = {key: v for key, v in ceil.items() if key not in ("read", "write", "copy", "encode_shape",
+                                                                                  "decode_shape")}
         rf["torch_copy_GB/s"] = device_copy_rate(dev)
     if not args.no_host:  # every rank, over its own PCIe link, at the same time
         own_rate, agg = host_inclusive(coder, k, m, L, min(B, 4096), dev, world)

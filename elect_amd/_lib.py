@@ -190,7 +190,8 @@ def unaligned_vector_ok() -> bool:
 
 def hbm_probe(kind: int, src: int, dst: int, nbytes: int, block: int = 256, waves_per_cu: int = 0,
               stream: int = 0) -> None:
-    """Enqueue one HBM ceiling probe (elect_ec_hbm_probe): kind 0 read, 1 write, 2 copy."""
+    """Enqueue one HBM ceiling probe (elect_ec_hbm_probe): kind 0 read, 1 write, 2 copy, 3 / 4 the
+    decode- / encode-shaped stream mixes (4 streams in, 1 / 2 out); | 0x100 for XCD-major order."""
     check(lib.elect_ec_hbm_probe(kind, src or None, dst, nbytes, block, waves_per_cu, stream or None), "hbm_probe")
 
 

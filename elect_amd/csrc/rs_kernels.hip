@@ -396,11 +396,18 @@ bool unaligned_vector_ok()
 }
 
 // HBM ceilings measured with the same access instructions as the coding
-// kernels (bench.py reports the coding kernels against them).
-template <int KIND>
+// kernels (bench.py reports the coding kernels against them).  KIND 0 read,
+// 1 write, 2 copy; 3 and 4 the coding kernels' stream mixes: four input streams
+// XORed into one (decode-shaped) or two (encode-shaped) output streams, each
+// `segs` segments long, the streams back to back in src / dst.  XCD: block b
+// takes the (b % 8)-th eighth of the range, in order (the dispatcher deals
+// blocks to the 8 XCDs round robin, so each XCD streams one contiguous eighth).
+template <int KIND, bool XCD>
 __global__ __launch_bounds__(kBlock) void hbm_probe_kernel(const uint8_t* in, uint8_t* out, uint64_t segs)
 {
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    uint64_t blk = blockIdx.x;
+    if constexpr (XCD) blk = (blk % 8) * (gridDim.x / 8) + blk / 8;
+    const uint64_t i = blk * blockDim.x + threadIdx.x;
     if (i >= segs) return;
     if constexpr (KIND == 0) {
         const uint4 v = load_nt(in + i * 16);
@@ -408,30 +415,53 @@ __global__ __launch_bounds__(kBlock) void hbm_probe_kernel(const uint8_t* in, ui
         if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9E3779B9u) reinterpret_cast<uint32_t*>(out)[threadIdx.x & 63u] = 1;
     } else if constexpr (KIND == 1) {
         store_nt(out + i * 16, make_uint4(static_cast<uint32_t>(i), 1u, 2u, 3u));
-    } else {
+    } else if constexpr (KIND == 2) {
         store_nt(out + i * 16, load_nt(in + i * 16));
+    } else {
+        uint4 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = load_nt(in + (j * segs + i) * 16);
+        const uint4 x = make_uint4(v[0].x ^ v[1].x ^ v[2].x ^ v[3].x, v[0].y ^ v[1].y ^ v[2].y ^ v[3].y,
+                                   v[0].z ^ v[1].z ^ v[2].z ^ v[3].z, v[0].w ^ v[1].w ^ v[2].w ^ v[3].w);
+        store_nt(out + i * 16, x);
+        if constexpr (KIND == 4) store_nt(out + (segs + i) * 16, make_uint4(x.x + 1u, x.y, x.z, x.w));
     }
+}
+
+template <int KIND>
+void launch_probe(bool xcd, uint64_t grid, int block, size_t lds, hipStream_t stream, const uint8_t* in, uint8_t* out,
+                  uint64_t segs)
+{
+    if (xcd)
+        hipLaunchKernelGGL((hbm_probe_kernel<KIND, true>), dim3(static_cast<uint32_t>(grid)), dim3(block), lds, stream, in,
+                           out, segs);
+    else
+        hipLaunchKernelGGL((hbm_probe_kernel<KIND, false>), dim3(static_cast<uint32_t>(grid)), dim3(block), lds, stream,
+                           in, out, segs);
 }
 
 hipError_t hbm_probe(int kind, const void* src, void* dst, size_t bytes, int block, int waves, hipStream_t stream)
 {
     (void)hipGetLastError();
-    if (kind < 0 || kind > 2 || bytes % 16 || (block != 64 && block != 128 && block != 256) || waves < 0 || !dst ||
+    const bool xcd = (kind & 0x100) != 0;
+    kind &= 0xFF;
+    if (kind < 0 || kind > 4 || bytes % 16 || (block != 64 && block != 128 && block != 256) || waves < 0 || !dst ||
         (kind != 1 && !src))
         return hipErrorInvalidValue;
     const uint64_t segs = bytes / 16;
     const uint64_t grid = (segs + block - 1) / block;
     if (grid == 0) return hipSuccess;
-    if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    if (grid > 0x7FFFFFFFull || (xcd && (grid % 8 || segs % block))) return hipErrorInvalidValue;
     const auto* in = static_cast<const uint8_t*>(src);
     auto* out = static_cast<uint8_t*>(dst);
     const size_t lds = cap_lds(block, 0, waves);
-    if (kind == 0)
-        hipLaunchKernelGGL(hbm_probe_kernel<0>, dim3(static_cast<uint32_t>(grid)), dim3(block), lds, stream, in, out, segs);
-    else if (kind == 1)
-        hipLaunchKernelGGL(hbm_probe_kernel<1>, dim3(static_cast<uint32_t>(grid)), dim3(block), lds, stream, in, out, segs);
-    else
-        hipLaunchKernelGGL(hbm_probe_kernel<2>, dim3(static_cast<uint32_t>(grid)), dim3(block), lds, stream, in, out, segs);
+    switch (kind) {
+    case 0: launch_probe<0>(xcd, grid, block, lds, stream, in, out, segs); break;
+    case 1: launch_probe<1>(xcd, grid, block, lds, stream, in, out, segs); break;
+    case 2: launch_probe<2>(xcd, grid, block, lds, stream, in, out, segs); break;
+    case 3: launch_probe<3>(xcd, grid, block, lds, stream, in, out, segs); break;
+    default: launch_probe<4>(xcd, grid, block, lds, stream, in, out, segs); break;
+    }
     return hipGetLastError();
 }
 

@@ -89,8 +89,13 @@ int elect_ec_unaligned_vector_ok(int* ok);
  * threads, at most waves_per_cu resident waves per CU (0: uncapped).
  * kind 0: read `bytes` of src (dst: a device buffer of >= 256 bytes that is
  * written only if the data hits a magic value); 1: write `bytes` of dst;
- * 2: copy `bytes` from src to dst.  bytes % 16 == 0.  No reference
- * counterpart: ELECT has no device path. */
+ * 2: copy `bytes` from src to dst; 3 / 4: the coding kernels' stream mixes,
+ * four `bytes`-long input streams back to back in src XORed into one (3,
+ * decode-shaped) or two (4, encode-shaped) output streams back to back in dst.
+ * kind | 0x100: XCD-major block order (each of the 8 XCDs streams one
+ * contiguous eighth; needs bytes / 16 a multiple of block and the block count
+ * a multiple of 8).  bytes % 16 == 0.  No reference counterpart: ELECT has no
+ * device path. */
 int elect_ec_hbm_probe(int kind, const void* src, void* dst, size_t bytes, int block, int waves_per_cu,
                        void* stream);
 
