@@ -146,12 +146,6 @@ struct LaunchPolicy {
     // The parity hash's per-wave sum weights each lane by 31^(16 lane) inside a DPP tree
     // (wave_poly31) instead of a per-lane table load that waits behind the parity stores.
     bool hash_dpp_weights = false;
-    // XCD-major block order for scalar-base plain launches (each of the 8 XCDs streams one
-    // contiguous eighth of the launch): 0 none, 1 wide shapes (>= 16 coefficients), 2 all.
-    // A 2 GiB read runs 6.9 -> 7.6 TB/s that way in 256-thread blocks (ceiling_probe.txt); in the
-    // product the RS(12,8) two-erasure decode went 84.7-85.0 -> 85.6-85.7 %, while the four-column
-    // shapes lost 2.4 % in XCD-major order (profiles/r04/xcd_order_ab.txt).
-    int xcd_order = 1;
 };
 
 #ifdef ELECT_EC_POLICY_HEADER
@@ -468,7 +462,6 @@ struct FastArgs {
     uint32_t hpow;          // 31^(hash offset of byte 0 of this launch window)
     uint32_t* hpart;        // per-wave partial sums [wave][R]: the wave's first stripe
     uint32_t* hpart_hi;     // assign mode: [wave][R] sums of a straddling wave's second stripe, else null
-    uint32_t xcd;           // 1: XCD-major block order (gridDim.x % 8 == 0; kPolicy.xcd_order)
     gf::PermTable tab[R][K];
 };
 
@@ -767,9 +760,7 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16u(const FastArgs<K, R> a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tl[R * K * kTabStride];
     __shared__ __attribute__((aligned(16))) uint8_t stage[LDSDMA ? K * 1024 : 16];  // (LDSDMA: one-wave blocks)
-    uint32_t blk = blockIdx.x;
-    if (a.xcd) blk = (blk & 7u) * (gridDim.x >> 3) + (blk >> 3);
-    const uint32_t idx = blk * blockDim.x + threadIdx.x;
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t first = __builtin_amdgcn_readfirstlane(idx);  // the wave's lane 0
     const uint32_t stripe = div_magic(first, a.magic, a.shift);  // wave-uniform
     const uint32_t off = (idx - stripe * a.segs) * 16u;
@@ -1161,8 +1152,6 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             const LaunchShape sh = launch_shape(a.hashes ? Family::kPlainHashed : Family::kPlain, K, R, p.len, scalar_base);
             const dim3 grid((a.total + sh.block - 1) / sh.block);
             const size_t lds = cap_lds(sh, kCoefs);
-            a.xcd = (kPolicy.xcd_order > 1 || (kPolicy.xcd_order == 1 && kCoefs >= 16)) && scalar_base &&
-                    grid.x % 8 == 0;
             if (!a.hashes) {
                 bool launched = false;
                 if constexpr (kPolicy.plain_lds_dma > 0) {  // one-wave launches load through LDS
