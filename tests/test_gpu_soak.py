@@ -47,8 +47,11 @@ def test_soak_every_iteration_verified(dev, oracle):
     coders = {}
     fails = []
     it = 0
-    t0 = time.perf_counter()
+    t0 = last = time.perf_counter()
     while time.perf_counter() - t0 < seconds or it < len(CASES):
+        if time.perf_counter() - last > 20:  # a long soak reports progress (a silent run looks hung)
+            last = time.perf_counter()
+            print(f"soak: {it} iterations, {last - t0:.0f} s, {len(fails)} failures", flush=True)
         k, m, L, B, layout, skew, era = CASES[it % len(CASES)]
         coder = coders.setdefault((k, m), RSCoder(k, m))
         args = types.SimpleNamespace(layout=layout, no_tiles=False, column_skew=skew)
