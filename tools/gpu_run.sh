@@ -248,7 +248,8 @@ for step in "$@"; do
                     -d $OUT/sqpmc_${cfg}_$pass -o run -- python3 bench.py $args || exit $?
             done
         done ;;
-    hostwait)  # host-path waits: blocking events + completion thread / polling events / round 3's callbacks (round 4)
+    hostwait)  # host-path waits: blocking events + completion thread / polling events / round 3's callbacks (round 4;
+               # the recipe of profiles/r04/hostwait_ab.txt: ELECT_EC_HOST_WAIT was removed with the losing modes)
         for i in 1 2; do for w in ${WAIT_MODES:-block spin callback}; do for T in ${WAIT_T:-1 16 64}; do
             ELECT_EC_HOST_WAIT=$w run "hostwait_${w}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
                 --host-op ${HOST_OP:-encode} --host-seconds ${HOST_S:-2} || exit $?
@@ -258,7 +259,8 @@ for step in "$@"; do
             ELECT_EC_HOST_WAIT=$w run "hostdirect_${al}_${w}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
                 --host-op ${HOST_OP:-encode} --host-seconds ${HOST_S:-2} --host-alloc $al || exit $?
         done; done; done; done ;;
-    directstreams)  # direct batches: per-unit DMAs on 1 or 2 streams (round 4)
+    directstreams)  # direct batches: per-unit DMAs on 1 or 2 streams (round 4; the recipe of direct_streams_ab.txt:
+                    # ELECT_EC_DIRECT_STREAMS was removed with the 2-stream variant)
         for i in 1 2; do for ds in 2 1; do for T in ${WAIT_T:-64 16 1}; do
             ELECT_EC_DIRECT_STREAMS=$ds run "directstreams_s${ds}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
                 --host-seconds ${HOST_S:-2} --host-alloc pinned || exit $?
@@ -270,7 +272,8 @@ for step in "$@"; do
             ELECT_EC_ZEROCOPY=$z run "pinzc_z${z}_$i" 300 python bench.py --config hostpath --threads 1 \
                 --host-seconds ${HOST_S:-2} --host-alloc pinned || exit $?
         done; done ;;
-    copyisa)  # pageable staging copies: AVX-512 vs SSE2 streaming stores (round 4)
+    copyisa)  # pageable staging copies: AVX-512 vs SSE2 streaming stores (round 4; the recipe of copy_isa_ab.txt:
+              # ELECT_EC_COPY_ISA was removed with the AVX-512 copies)
         for i in 1 2; do for isa in avx512 sse; do for T in ${WAIT_T:-64 16 1}; do
             ELECT_EC_COPY_ISA=$isa run "copyisa_${isa}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
                 --host-seconds ${HOST_S:-2} || exit $?
