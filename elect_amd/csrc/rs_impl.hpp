@@ -972,11 +972,15 @@ constexpr int lens_unroll() { return K <= 4 ? 2 : 1; }
     const uint32_t s = t / rows, r = t % rows, lane = threadIdx.x & 63u;
     const uint64_t start = static_cast<uint64_t>(s) * segs;
     uint32_t sum = 0;
+    // Unrolled so that a lane keeps several partial loads in flight: an ELECT-size unit
+    // (4.4 MB in 64 KiB tiles) has 4,352 partials per row, 68 per lane.
     if (hi) {
         const uint64_t w0 = start / 64, w1 = (start + segs - 1) / 64;
+#pragma unroll 8
         for (uint64_t w = w0 + lane; w <= w1; w += 64) sum += (w * 64 >= start ? part : hi)[w * rows + r];
     } else {
         const uint64_t w0 = (start + 63) / 64, w1 = (start + segs) / 64;
+#pragma unroll 8
         for (uint64_t w = w0 + lane; w < w1; w += 64) sum += part[w * rows + r];
     }
     sum = wave_sum(sum);
