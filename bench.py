@@ -173,6 +173,9 @@ def parse():
                     help="hostpath: the callers' buffers are ordinary memory (ELECT's ByteBuffer.allocateDirect), or "
                          "elect_ec_host_alloc buffers (page-locked; the batcher then moves them by DMA, no staging "
                          "copies: INTEGRATION.md, host buffers)")
+    ap.add_argument("--host-register", type=int, choices=(0, 1), default=None,
+                    help="hostpath: ELECT_EC_REGISTER for the run (1: batched callers' pageable units page-locked "
+                         "per call, their interior pages moved by DMA; default: the library's default)")
     ap.add_argument("--host-op", choices=("encode", "encode_ex"), default="encode",
                     help="hostpath: plain encode (the JNI encodeImpl), or ELECT's fused encode step "
                          "(encodeExImpl: content = codeLength/1.05, parity hashCodes)")
@@ -975,6 +978,8 @@ def config_hostpath(args, world, rank, dev):
     from elect_amd import _lib
     k, m, L = 4, 2, args.host_chunk
     T = args.threads
+    if args.host_register is not None:  # read by the library at its first host call
+        os.environ["ELECT_EC_REGISTER"] = str(args.host_register)
     coder = RSCoder(k, m)
     _lib.set_batching(args.batch)
     ndev = max(1, args.host_devices)
@@ -1067,6 +1072,7 @@ def config_hostpath(args, world, rank, dev):
     return {"metric": f"GiB/s host-memory RS(6,4) {op_name} through the C ABI (JNI calling convention)",
             "value": round(data_gib / dt, 2), "unit": "GiB/s", "n_gpus": world,
             "devices": ndev, "callers": T, "host_path_stats": stats, "host_alloc": args.host_alloc,
+            "host_register": os.environ.get("ELECT_EC_REGISTER", "library default"),
             # CPU time the whole process spent (every caller, helper and dispatcher thread) per GiB
             # of data coded: what the offload costs the node's cores
             "cpu_core_ms_per_GiB": round(core_ms, 2),

@@ -133,6 +133,21 @@ SIGNATURES = [
                                             ctypes.POINTER(ColumnT), _cp]),
 ]
 
+# One HIP runtime per process.  PyTorch-ROCm bundles its own libamdhip64 /
+# libhsa-runtime64 (torch/lib) under the same sonames as /opt/rocm's, which the
+# library links.  Loaded first, the library pulls in /opt/rocm's runtime; torch,
+# imported later, then loads its own copy beside it (its libraries name the
+# unversioned file), and whichever of the two HSA runtimes initialises second
+# finds no device: round 5 saw elect_ec_host_alloc's hipHostMalloc fail with
+# "no ROCm-capable device is detected" in a test module that imported this
+# module before torch.  Importing torch first (where it is installed) makes
+# the library bind to torch's already-loaded runtime, as every torch-first
+# process already did.  (A JVM loads only the library's own runtime.)
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"{LIB_PATH} is missing: build the MI355X engine first "
                       "(python -m elect_amd.build) — there is no CPU fallback")
@@ -209,10 +224,12 @@ def set_batching(enable: bool, window_us: int = 0, arena_bytes: int = 256 << 20)
 
 def host_path_stats() -> dict:
     """The host-memory path's counters (elect_ec_host_path_stats)."""
-    out = (ctypes.c_uint64 * 5)()
-    lib.elect_ec_host_path_stats(out, 5)
+    out = (ctypes.c_uint64 * 11)()
+    lib.elect_ec_host_path_stats(out, 11)
     return {"zero_copy": out[0], "zero_copy_fallback": out[1], "batched": out[2], "per_thread": out[3],
-            "direct": out[4]}
+            "direct": out[4], "registered": out[5], "register_fallback": out[6], "unregister_failures": out[7],
+            "register_cpu_ms": round(out[8] * 1e-6, 1), "unregister_cpu_ms": round(out[9] * 1e-6, 1),
+            "dispatch_issue_cpu_ms": round(out[10] * 1e-6, 1)}
 
 
 def host_alloc(nbytes: int) -> int:

@@ -107,7 +107,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, units()))
     tmp = LIB + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-L/opt/rocm/lib", "-lhsa-runtime64"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed\n{r.stderr}")

@@ -3,13 +3,18 @@
 // (EC/NativeRSEncoder.c:43-61 -> EC/erasure_coder.c:74-98).
 #include "host_path.hpp"
 
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
 #include <emmintrin.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
+#include <ctime>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -103,20 +108,31 @@ public:
                 void* p = it->second.back();
                 it->second.pop_back();
                 free_bytes_ -= cls;
-                live_[reinterpret_cast<uintptr_t>(p)] = Block{cls, true};
+                live_[reinterpret_cast<uintptr_t>(p)] = Block{cls, true, delta_[p]};
                 return p;
             }
         }
         void* p = nullptr;
-        bool pinned = hipHostMalloc(&p, cls, hipHostMallocPortable) == hipSuccess && p;
+        const hipError_t e = hipHostMalloc(&p, cls, hipHostMallocPortable);
+        bool pinned = e == hipSuccess && p;
         if (!pinned) {
+            if (std::getenv("ELECT_EC_DEBUG"))
+                std::fprintf(stderr, "elect_ec_host_alloc: hipHostMalloc(%zu) failed: %s\n", cls, hipGetErrorString(e));
             (void)hipGetLastError();
             p = std::aligned_alloc(4096, cls);
             if (!p) return nullptr;
         }
+        intptr_t delta = 0;  // device address - host address (the batches' kernels read the units there)
+        if (pinned) {
+            void* d = nullptr;
+            if (hipHostGetDevicePointer(&d, p, 0) == hipSuccess)
+                delta = reinterpret_cast<intptr_t>(d) - reinterpret_cast<intptr_t>(p);
+            (void)hipGetLastError();
+        }
         try {
             std::unique_lock<std::shared_mutex> lock(mu_);
-            live_[reinterpret_cast<uintptr_t>(p)] = Block{cls, pinned};
+            live_[reinterpret_cast<uintptr_t>(p)] = Block{cls, pinned, delta};
+            if (pinned) delta_[p] = delta;
         } catch (...) {  // no record, no buffer: nothing leaks
             if (pinned)
                 (void)hipHostFree(p);
@@ -164,6 +180,17 @@ public:
         return it->second.pinned && a + n <= it->first + it->second.size;
     }
 
+    // Device address of p (inside a live page-locked block).
+    uintptr_t device_addr(const void* p) const
+    {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        std::shared_lock<std::shared_mutex> lock(mu_);
+        auto it = live_.upper_bound(a);
+        if (it == live_.begin()) return a;
+        --it;
+        return a + static_cast<uintptr_t>(it->second.delta);
+    }
+
     bool any() const
     {
         std::shared_lock<std::shared_mutex> lock(mu_);
@@ -175,6 +202,7 @@ private:
     struct Block {
         size_t size = 0;
         bool pinned = false;
+        intptr_t delta = 0;  // device address - host address
     };
 
     // free page-locked bytes kept for reuse (ELECT_EC_HOST_POOL_MB, default 4096)
@@ -190,22 +218,417 @@ private:
     mutable std::shared_mutex mu_;
     std::map<uintptr_t, Block> live_;
     std::map<size_t, std::vector<void*>> free_;
+    std::map<void*, intptr_t> delta_;  // every page-locked block ever made (blocks are only ever reused)
     size_t free_bytes_ = 0;
 };
 
-// Every byte the call reads and writes lies in page-locked pool buffers.
+// Bytes of input j the kernels may touch when they read the unit where it lies
+// (zero-copy): a padded unit's content rounded up to the 16-byte segment, never
+// past the unit.  The padded vector kernel loads the whole segment that holds a
+// content end (rs_impl.hpp, gf_apply_x16<PAD>) and masks it: up to 15 bytes
+// past lens[j], which on a caller pointer off 16-byte alignment can cross into
+// memory that is neither registered nor in the pool.
+size_t input_span(const HostOp& op, int j, size_t len)
+{
+    if (!op.lens) return len;
+    return std::min(len, (op.lens[j] + 15) & ~size_t{15});
+}
+
+// Every byte the call's kernels may touch lies in page-locked pool buffers
+// (inputs: input_span, so a zero-copy kernel reading a pool unit in place stays
+// inside its block).
 bool direct_op(const HostOp& op, size_t len)
 {
     PinnedPool& pool = PinnedPool::get();
     if (!pool.any()) return false;
     for (int j = 0; j < op.cols; ++j) {
         const size_t n = op.lens ? op.lens[j] : len;
-        if (n && !pool.pinned(op.in[j], n)) return false;
+        if (n && !pool.pinned(op.in[j], input_span(op, j, len))) return false;
     }
     for (int r = 0; r < op.rows; ++r)
         if (!pool.pinned(op.out[r], len)) return false;
     return true;
 }
+
+// ---------------------------------------------------------------------------
+// Page-locking callers' own (pageable) memory for one call: hipHostRegister,
+// process-wide, through one registry.
+//
+// Round 4 ran batched callers' units registered per call and the GPU suite
+// faulted (hipErrorIllegalAddress) in a later device-only test.  The cause,
+// measured on the box (tools/tune/register_overlap_probe.cpp,
+// profiles/r05/register_overlap.txt): the HIP runtime ACCEPTS a registration
+// whose pages overlap a live one, in every arrangement (one range inside
+// another, shifted, identical), and maps both at the same device address (the
+// host address).  The first hipHostUnregister then removes the shared pages'
+// mapping and bookkeeping while the other registration is still in use: after
+// an identical range was registered twice, the second unregister returns
+// hipErrorHostMemoryNotRegistered (the first took both down), and after
+// shifted overlaps the runtime's object map is left corrupt, so that a later,
+// unrelated unregister aborts the process ("Memobj map does not have ptr").
+// Round 4 registered each call's page-ROUNDED ranges: ELECT's units (and the
+// tests' numpy arrays) sit back to back on the heap, so a unit's first and last
+// pages are shared with its neighbours, and concurrent callers registered
+// overlapping ranges; a call finishing first unmapped pages another call's
+// DMAs still read.  The same hazard sat in the zero-copy path below
+// (host_path.cpp round 4: merged page-rounded ranges, released by base).
+// Two more facts from the probe: a DMA whose host range spans two adjacent
+// registrations is refused (hipErrorInvalidValue), and hipHostUnregister
+// given an interior pointer aborts the process.
+//
+// So: (1) no two live registrations share a page — a request that meets a
+// live registration of another extent is refused here, before the runtime
+// sees it; an identical request shares the live registration (refcounted);
+// (2) every registration is released by the exact base it was made with,
+// after the last DMA or kernel using it has completed (callers release after
+// their batch's completion); (3) memory another party has registered (either
+// end of the range already known to the runtime) is never registered again;
+// (4) a failed unregister is counted (host_path_stats), never ignored
+// silently.  The batched path registers only the pages lying wholly inside a
+// unit (interior pages): those belong to that unit alone, so neighbours never
+// meet, and the <= 2 partial pages at its ends travel through the arena.
+// ---------------------------------------------------------------------------
+std::atomic<uint64_t> g_unregister_failures{0};
+// CPU time (ns, calling threads) spent registering, unregistering, and in the
+// dispatchers' issue() (host_path_stats entries 8-10, for the A/B of this path).
+std::atomic<uint64_t> g_register_cpu_ns{0}, g_unregister_cpu_ns{0}, g_issue_cpu_ns{0};
+
+uint64_t thread_cpu_ns()
+{
+    timespec t{};
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &t);
+    return static_cast<uint64_t>(t.tv_sec) * 1000000000ull + static_cast<uint64_t>(t.tv_nsec);
+}
+
+// The HSA agent of HIP device `dev` (matched by PCI location), for
+// hsa_amd_memory_lock.  False when it cannot be found.
+bool hsa_agent_of(int dev, hsa_agent_t* out)
+{
+    struct Found {
+        uint32_t bdf = 0, domain = 0;
+        bool ok = false;
+        hsa_agent_t agent{};
+    };
+    static std::mutex mu;
+    static std::map<int, hsa_agent_t> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(dev);
+    if (it != cache.end()) {
+        *out = it->second;
+        return true;
+    }
+    static const bool init = hsa_init() == HSA_STATUS_SUCCESS;  // (reference counted: the HIP runtime holds one)
+    if (!init) return false;
+    int bus = 0, device = 0, domain = 0;
+    if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&device, hipDeviceAttributePciDeviceId, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&domain, hipDeviceAttributePciDomainID, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    Found f;
+    f.bdf = (static_cast<uint32_t>(bus) << 8) | (static_cast<uint32_t>(device) << 3);
+    f.domain = static_cast<uint32_t>(domain);
+    hsa_iterate_agents(
+        [](hsa_agent_t a, void* arg) -> hsa_status_t {
+            auto* f = static_cast<Found*>(arg);
+            hsa_device_type_t t{};
+            uint32_t bdf = 0, domain = 0;
+            if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+                return HSA_STATUS_SUCCESS;
+            hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
+            hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &domain);
+            if ((bdf & ~7u) != f->bdf || domain != f->domain) return HSA_STATUS_SUCCESS;
+            f->agent = a;
+            f->ok = true;
+            return HSA_STATUS_INFO_BREAK;
+        },
+        &f);
+    if (!f.ok) return false;
+    cache[dev] = f.agent;
+    *out = f.agent;
+    return true;
+}
+
+class Registrar {
+public:
+    // kHipRegister: hipHostRegister(Mapped) — the zero-copy path; the HIP
+    // runtime's own transfers know the pages.  Its hipHostUnregister waits for
+    // every queued operation on the device, other streams included (7.1 ms
+    // behind another stream's 7.1 ms of copies, profiles/r05/register_overlap.txt
+    // part 3), which is why per-call hipHostRegister cannot serve concurrent
+    // callers: at 64 callers the unregister waits cost 485 core-ms per GiB.
+    // kHsaLock: hsa_amd_memory_lock for the calling device's agent — the
+    // batched path's kernels read and write the pages through the returned
+    // address; hsa_amd_memory_unlock does not wait for the device (part 4).
+    enum Kind { kHipRegister, kHsaLock };
+
+    static Registrar& get()
+    {
+        static Registrar* r = new Registrar();  // never destroyed: registrations may be in use at exit
+        return *r;
+    }
+
+    // A reference on a registration of exactly [lo, hi) (page aligned, lo < hi)
+    // of this kind: the identical live one, or a new one.  False (nothing held)
+    // when [lo, hi) shares a page with a registration of another extent or
+    // kind, or with memory the HIP runtime already knows, or when the runtime
+    // refuses.  *dev_lo: the device address of lo (kHsaLock).  A kHipRegister
+    // registration is made with hipHostRegisterMapped and its device pointer
+    // is looked up at once.
+    bool acquire(uintptr_t lo, uintptr_t hi, Kind kind, int dev = 0, uintptr_t* dev_lo = nullptr)
+    {
+        std::unique_lock<std::mutex> lock(mu_);
+        for (;;) {
+            Entry* same = nullptr;
+            auto next = live_.upper_bound(lo);  // first registration starting after lo
+            if (next != live_.end() && next->first < hi) return false;
+            if (next != live_.begin()) {
+                auto prev = std::prev(next);
+                if (prev->second.end > lo) {
+                    if (prev->first != lo || prev->second.end != hi || prev->second.kind != kind) return false;
+                    same = &prev->second;
+                }
+            }
+            if (!same) break;
+            if (same->state == Entry::kLive) {
+                ++same->refs;
+                if (dev_lo) *dev_lo = same->dev_lo;
+                return true;
+            }
+            if (same->state == Entry::kRetiring) return false;
+            changed_.wait(lock);  // its maker is registering it: wait for the outcome
+        }
+        live_.emplace(lo, Entry{hi, 0, Entry::kPending, kind, 0});
+        lock.unlock();
+        const uint64_t t0 = thread_cpu_ns();
+        void* p = reinterpret_cast<void*>(lo);
+        uintptr_t d_lo = 0;
+        bool ok = false;
+        if (kind == kHsaLock) {
+            hsa_agent_t agent{};
+            void* ap = nullptr;
+            ok = hsa_agent_of(dev, &agent) && !known(lo) && !known(hi - 1) &&
+                 hsa_amd_memory_lock(p, hi - lo, &agent, 1, &ap) == HSA_STATUS_SUCCESS;
+            d_lo = reinterpret_cast<uintptr_t>(ap);
+        } else {
+            ok = !known(lo) && !known(hi - 1) && hipHostRegister(p, hi - lo, hipHostRegisterMapped) == hipSuccess;
+            void* d = nullptr;  // creates the device mapping now
+            if (ok && hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+                if (hipHostUnregister(p) != hipSuccess) g_unregister_failures.fetch_add(1);
+                ok = false;
+            }
+            d_lo = reinterpret_cast<uintptr_t>(d);
+            (void)hipGetLastError();  // a refused registration is not the thread's next call's error
+        }
+        g_register_cpu_ns.fetch_add(thread_cpu_ns() - t0);
+        lock.lock();
+        auto it = live_.find(lo);
+        if (ok) {
+            it->second.state = Entry::kLive;
+            it->second.refs = 1;
+            it->second.dev_lo = d_lo;
+            if (dev_lo) *dev_lo = d_lo;
+        } else {
+            live_.erase(it);
+        }
+        changed_.notify_all();
+        return ok;
+    }
+
+    // Drops a reference taken by acquire(lo, ...); the last one unregisters
+    // (by lo, the base it was registered with).  Only after every transfer and
+    // kernel touching the pages has completed.
+    void release(uintptr_t lo)
+    {
+        std::unique_lock<std::mutex> lock(mu_);
+        auto it = live_.find(lo);
+        if (it == live_.end() || it->second.state != Entry::kLive) return;
+        if (--it->second.refs > 0) return;
+        it->second.state = Entry::kRetiring;  // stays in the map (refusing overlaps) until it is gone
+        const Kind kind = it->second.kind;
+        lock.unlock();
+        const uint64_t t0 = thread_cpu_ns();
+        const bool ok = kind == kHsaLock ? hsa_amd_memory_unlock(reinterpret_cast<void*>(lo)) == HSA_STATUS_SUCCESS
+                                         : hipHostUnregister(reinterpret_cast<void*>(lo)) == hipSuccess;
+        if (!ok) {
+            g_unregister_failures.fetch_add(1);
+            (void)hipGetLastError();
+        }
+        g_unregister_cpu_ns.fetch_add(thread_cpu_ns() - t0);
+        lock.lock();
+        live_.erase(lo);
+        changed_.notify_all();
+    }
+
+private:
+    struct Entry {
+        uintptr_t end;
+        int refs;
+        enum State { kPending, kLive, kRetiring } state;
+        Kind kind;
+        uintptr_t dev_lo;
+    };
+
+    // The HIP runtime already knows this address (registered or allocated by anyone).
+    static bool known(uintptr_t a)
+    {
+        hipPointerAttribute_t attr{};
+        const hipError_t e = hipPointerGetAttributes(&attr, reinterpret_cast<void*>(a));
+        (void)hipGetLastError();
+        return e != hipSuccess || attr.type != hipMemoryTypeUnregistered;
+    }
+
+    std::mutex mu_;
+    std::condition_variable changed_;
+    std::map<uintptr_t, Entry> live_;  // disjoint page ranges, keyed by base
+};
+
+// Callers locking or unlocking their units at once (ELECT_EC_REGISTER_SLOTS,
+// default 8): hsa_amd_memory_lock / unlock contend in the driver (round 5,
+// lock + unlock of 4.4 MB units: 4.7 core-ms per GiB from 8 threads, 21.7 from
+// 64, profiles/r05/register_overlap.txt part 4), so the rest wait their turn.
+class RegisterSlots {
+public:
+    static RegisterSlots& get()
+    {
+        static RegisterSlots s;
+        return s;
+    }
+    void take()
+    {
+        std::unique_lock<std::mutex> lock(mu_);
+        cv_.wait(lock, [&] { return free_ > 0; });
+        --free_;
+    }
+    void give()
+    {
+        {
+            std::lock_guard<std::mutex> lock(mu_);
+            ++free_;
+        }
+        cv_.notify_one();
+    }
+
+private:
+    RegisterSlots()
+    {
+        const char* e = std::getenv("ELECT_EC_REGISTER_SLOTS");
+        free_ = e ? std::max(1, std::atoi(e)) : 8;
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    int free_ = 8;
+};
+
+// How a direct call's units move (Batcher, direct batches).  Unit bytes
+// [lo, hi) are read (written) by the batch's gather (scatter) kernel straight
+// from (to) the caller's memory at device address *_dev (the address of byte
+// lo); the rest of the unit ([0, lo) and [hi, n)) goes through the arena,
+// copied by the caller.  Pool units: all of it direct.  Locked units: their
+// interior pages.
+struct DirectPlan {
+    bool direct = false;
+    size_t in_lo[kern::kMaxCols] = {}, in_hi[kern::kMaxCols] = {};
+    size_t out_lo[kern::kMaxRows] = {}, out_hi[kern::kMaxRows] = {};
+    uintptr_t in_dev[kern::kMaxCols] = {}, out_dev[kern::kMaxRows] = {};
+    uintptr_t held[kern::kMaxCols + kern::kMaxRows] = {};  // locks to release
+    int nheld = 0;
+};
+
+// Direct batches move their units by gather / scatter kernels (the default) or,
+// with ELECT_EC_DIRECT_MOVE=dma, by a hipMemcpyAsync per piece (round 4's way;
+// page-locked pool units only: no per-call locking then).
+bool direct_by_kernel()
+{
+    static const bool k = [] {
+        const char* e = std::getenv("ELECT_EC_DIRECT_MOVE");
+        return !(e && std::string(e) == "dma");
+    }();
+    return k;
+}
+
+// Per-call page locking of batched callers' pageable units (ELECT_EC_REGISTER:
+// 0 off, 1 on, the default; units of at least kMinBytes): each unit's interior
+// pages are locked with hsa_amd_memory_lock (Registrar::kHsaLock), the batch's
+// kernels move them over PCIe, and they are unlocked when the call's batch is
+// done.  No staging copies of the interior, no DMA engine, no device wait.
+struct RegisterPath {
+    static constexpr size_t kMinBytes = size_t{1} << 20;
+    static constexpr uintptr_t kPage = 4096;
+    static constexpr uintptr_t kMinInterior = kPage * 16;  // shorter: all of the unit through the arena
+
+    static int mode()
+    {
+        static const int m = [] {
+            const char* e = std::getenv("ELECT_EC_REGISTER");
+            return e ? std::atoi(e) : 1;
+        }();
+        return m;
+    }
+
+    // Interior pages of [p, p + n): [lo, hi) page aligned (lo == hi: none).
+    static void interior(const void* p, size_t n, uintptr_t& lo, uintptr_t& hi)
+    {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        lo = (a + kPage - 1) & ~(kPage - 1);
+        hi = (a + n) & ~(kPage - 1);
+        if (hi < lo) hi = lo;
+    }
+
+    // Locks every unit's interior pages (one lock per unit; units with equal
+    // interiors share it).  False (nothing held): take the staged path.
+    static bool plan(const HostOp& op, size_t len, int dev, DirectPlan& dp)
+    {
+        if (mode() != 1 || len < kMinBytes || !direct_by_kernel()) return false;
+        RegisterSlots& slots = RegisterSlots::get();
+        slots.take();
+        Registrar& reg = Registrar::get();
+        bool ok = true;
+        PinnedPool& pool = PinnedPool::get();
+        auto add = [&](const void* p, size_t n, size_t& lo_off, size_t& hi_off, uintptr_t& dev_addr) {
+            lo_off = hi_off = 0;
+            if (!ok || !p || !n) return;
+            if (pool.pinned(p, n)) {  // a pool unit among pageable ones: all of it in place, no lock
+                hi_off = n;
+                dev_addr = pool.device_addr(p);
+                return;
+            }
+            uintptr_t lo = 0, hi = 0;
+            interior(p, n, lo, hi);
+            if (hi - lo < kMinInterior) return;
+            if (!reg.acquire(lo, hi, Registrar::kHsaLock, dev, &dev_addr)) {
+                ok = false;
+                return;
+            }
+            dp.held[dp.nheld++] = lo;
+            const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+            lo_off = lo - a;
+            hi_off = hi - a;
+            dev_addr -= lo_off;  // the unit's base, at its device address (only [lo, hi) is read there)
+        };
+        for (int j = 0; j < op.cols; ++j)
+            add(op.in[j], op.lens ? op.lens[j] : len, dp.in_lo[j], dp.in_hi[j], dp.in_dev[j]);
+        for (int r = 0; r < op.rows; ++r) add(op.out[r], len, dp.out_lo[r], dp.out_hi[r], dp.out_dev[r]);
+        if (!ok) {
+            for (int i = 0; i < dp.nheld; ++i) reg.release(dp.held[i]);
+            dp.nheld = 0;
+        }
+        slots.give();
+        dp.direct = ok;
+        return ok;
+    }
+
+    static void release(DirectPlan& dp)
+    {
+        if (!dp.nheld) return;
+        RegisterSlots& slots = RegisterSlots::get();
+        slots.take();
+        for (int i = 0; i < dp.nheld; ++i) Registrar::get().release(dp.held[i]);
+        slots.give();
+        dp.nheld = 0;
+    }
+};
 
 // Copy fan-out for lone callers.  One thread's staging copies (~20 GB/s) bound a
 // caller that has the device to itself: a 4.4 MB RS(6,4) stripe moves 26 MB
@@ -632,11 +1055,14 @@ public:
 
     explicit Batcher(int dev) : dev_(dev) {}
 
-    // direct: every unit of the call lies in page-locked pool memory (direct_op);
-    // its units then move by DMA between the caller's buffers and the device,
-    // with no staging copies, in batches of direct calls only.
-    int submit(const HostOp& op, size_t len, bool direct)
+    // dp (a direct call, dp->direct): its units move by DMA between the caller's
+    // page-locked memory (pool buffers, or units registered for the call) and
+    // the device, with no staging copies, in batches of direct calls only;
+    // bytes outside a unit's [lo, hi) (a registered unit's partial end pages)
+    // go through the arena, copied by this caller.  nullptr: staged.
+    int submit(const HostOp& op, size_t len, const DirectPlan* dp)
     {
+        const bool direct = dp && dp->direct;
         struct InFlight {  // callers inside submit(), for the copy fan-out policy
             std::atomic<int>& n;
             explicit InFlight(std::atomic<int>& c) : n(c) { n.fetch_add(1); }
@@ -705,19 +1131,32 @@ public:
         for (int j = 0; j < op.cols; ++j) {
             const size_t n = op.lens ? op.lens[j] : len;  // padded: only the content bytes
             if (op.lens) slab->pin_lens[static_cast<size_t>(slot) * op.cols + j] = static_cast<uint32_t>(n);
-            if (direct) {  // the dispatcher DMAs it from the caller's buffer
-                slab->dsrc[static_cast<size_t>(slot) * kern::kMaxCols + j] = n ? op.in[j] : nullptr;
-                slab->dsrc_n[static_cast<size_t>(slot) * kern::kMaxCols + j] = n;
+            if (direct) {  // the dispatcher DMAs [lo, hi) from the caller's buffer, the rest from the arena
+                const size_t i = static_cast<size_t>(slot) * kern::kMaxCols + j;
+                const size_t lo = std::min(dp->in_lo[j], n), hi = std::min(std::max(dp->in_hi[j], lo), n);
+                // the unit's base at its device address ([lo, hi) is what the gather reads there)
+                slab->dsrc[i] = n ? reinterpret_cast<const uint8_t*>(dp->in_dev[j]) : nullptr;
+                slab->dsrc_n[i] = n;
+                slab->dsrc_lo[i] = lo;
+                slab->dsrc_hi[i] = hi;
+                uint8_t* const at = in_base + j * pitch;  // untiled
+                if (lo) add_copy(jobs, at, op.in[j], lo);
+                if (hi < n) add_copy(jobs, at + hi, op.in[j] + hi, n - hi);
                 continue;
             }
             for (size_t o = 0; o < n; o += pitch)  // untiled: pitch >= len, one copy
                 add_copy(jobs, in_base + (o / pitch * op.cols + j) * pitch, op.in[j] + o, std::min(pitch, n - o));
         }
         if (direct) {
-            for (int r = 0; r < op.rows; ++r) slab->ddst[static_cast<size_t>(slot) * kern::kMaxRows + r] = op.out[r];
-        } else {
-            run_copies(jobs, callers_.load() <= lone_callers());  // fenced before the dispatcher's H2D reads them
+            for (int r = 0; r < op.rows; ++r) {
+                const size_t i = static_cast<size_t>(slot) * kern::kMaxRows + r;
+                const size_t lo = std::min(dp->out_lo[r], len);
+                slab->ddst[i] = reinterpret_cast<uint8_t*>(dp->out_dev[r]);
+                slab->ddst_lo[i] = lo;
+                slab->ddst_hi[i] = std::min(std::max(dp->out_hi[r], lo), len);
+            }
         }
+        if (!jobs.empty()) run_copies(jobs, !direct && callers_.load() <= lone_callers());  // fenced before the H2D
 
         lock.lock();
         if (++slab->filled == slab->reserved) cv_worker_.notify_one();
@@ -725,7 +1164,16 @@ public:
         const int status = slab->status;
         lock.unlock();
 
-        if (status == ELECT_EC_OK && !direct) {  // (direct: the D2H wrote the caller's buffers)
+        if (status == ELECT_EC_OK && direct) {  // the D2H wrote [lo, hi) of each output; the rest is in the arena
+            const uint8_t* const out_base = slab->pin_out + slot * (op.rows * pitch);
+            jobs.clear();
+            for (int r = 0; r < op.rows; ++r) {
+                const size_t lo = std::min(dp->out_lo[r], len), hi = std::min(std::max(dp->out_hi[r], lo), len);
+                if (lo) add_copy(jobs, op.out[r], out_base + r * pitch, lo);
+                if (hi < len) add_copy(jobs, op.out[r] + hi, out_base + r * pitch + hi, len - hi);
+            }
+            if (!jobs.empty()) run_copies(jobs, false);
+        } else if (status == ELECT_EC_OK) {
             const size_t out_stride = tiles * op.rows * pitch;
             const uint8_t* const out_base = slab->pin_out + slot * out_stride;
             jobs.clear();
@@ -763,8 +1211,9 @@ private:
     // profiles/r04/tsan_summary.txt).
     struct DirectSlots {
         std::vector<const uint8_t*> src;
-        std::vector<size_t> src_n;
+        std::vector<size_t> src_n, src_lo, src_hi;
         std::vector<uint8_t*> dst;
+        std::vector<size_t> dst_lo, dst_hi;
     };
 
     struct Slab {
@@ -781,12 +1230,20 @@ private:
         uint8_t *pin_in = nullptr, *pin_out = nullptr, *d_in = nullptr, *d_out = nullptr;
         uint32_t *pin_lens = nullptr, *d_lens = nullptr;  // [slot][cols]
         int32_t *pin_hash = nullptr, *d_hash = nullptr;    // [slot][rows]
+        // direct batches: the arenas' device addresses, and the gather + scatter
+        // piece table (page-locked, read by the copy kernels where it lies)
+        uint8_t *pin_in_dev = nullptr, *pin_out_dev = nullptr;
+        kern::CopyPiece* pieces = nullptr;
+        const kern::CopyPiece* pieces_dev = nullptr;
+        size_t max_pieces = 0;
         uint32_t* d_scratch = nullptr;                       // hash partials of the batch's launch
         size_t scratch_words = 0;
-        // direct batches: each slot's unit pointers and input byte counts, [slot][kMaxCols / kMaxRows]
+        // direct batches: each slot's unit pointers, input byte counts and the
+        // [lo, hi) moved straight from / to the caller's memory, [slot][kMaxCols / kMaxRows]
         std::unique_ptr<const uint8_t*[]> dsrc;
-        std::unique_ptr<size_t[]> dsrc_n;
+        std::unique_ptr<size_t[]> dsrc_n, dsrc_lo, dsrc_hi;
         std::unique_ptr<uint8_t*[]> ddst;
+        std::unique_ptr<size_t[]> ddst_lo, ddst_hi;
         std::condition_variable done;  // this batch's callers wait here for kDone
         hipStream_t stream = nullptr;
         hipEvent_t h2d_done = nullptr;
@@ -844,7 +1301,13 @@ private:
         for (Slab& s : active()) {
             s.owner = this;
             hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming);
+            // ELECT_EC_DISPATCH_BLOCKING=1: the dispatcher sleeps on the event instead of polling it (A/B)
+            static const bool blocking = [] {
+                const char* b = std::getenv("ELECT_EC_DISPATCH_BLOCKING");
+                return b && std::atoi(b) > 0;
+            }();
+            if (e == hipSuccess)
+                e = hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming | (blocking ? hipEventBlockingSync : 0));
             // device first: an arena too large for the device fails there, before any host pinning
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_in), arena);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_out), arena);
@@ -854,18 +1317,36 @@ private:
             if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_lens), meta, hipHostMallocDefault);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_lens), meta);
             if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_hash), meta, hipHostMallocDefault);
+            // gather: <= one piece per 64 KiB of the arena plus 3 per unit; the scatter as many
+            s.max_pieces = 2 * (arena / kern::kMaxPieceBytes + 3 * kMaxDirectSlots * std::max(kern::kMaxCols, kern::kMaxRows));
+            if (e == hipSuccess)
+                e = hipHostMalloc(reinterpret_cast<void**>(&s.pieces), s.max_pieces * sizeof(kern::CopyPiece),
+                                  hipHostMallocDefault);
+            void* dv = nullptr;
+            if (e == hipSuccess) e = hipHostGetDevicePointer(&dv, s.pieces, 0);
+            s.pieces_dev = static_cast<const kern::CopyPiece*>(dv);
+            if (e == hipSuccess) e = hipHostGetDevicePointer(&dv, s.pin_in, 0);
+            s.pin_in_dev = static_cast<uint8_t*>(dv);
+            if (e == hipSuccess) e = hipHostGetDevicePointer(&dv, s.pin_out, 0);
+            s.pin_out_dev = static_cast<uint8_t*>(dv);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_hash), meta);
             s.scratch_words = kern::hash_scratch_need(arena / 16);  // a batch has at most arena/16 segments
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_scratch), s.scratch_words * sizeof(uint32_t));
             if (e != hipSuccess) return map_hip(e);
             s.dsrc.reset(new (std::nothrow) const uint8_t*[kMaxDirectSlots * kern::kMaxCols]);
             s.dsrc_n.reset(new (std::nothrow) size_t[kMaxDirectSlots * kern::kMaxCols]);
+            s.dsrc_lo.reset(new (std::nothrow) size_t[kMaxDirectSlots * kern::kMaxCols]);
+            s.dsrc_hi.reset(new (std::nothrow) size_t[kMaxDirectSlots * kern::kMaxCols]);
             s.ddst.reset(new (std::nothrow) uint8_t*[kMaxDirectSlots * kern::kMaxRows]);
-            if (!s.dsrc || !s.dsrc_n || !s.ddst) return ELECT_EC_ENOMEM;
+            s.ddst_lo.reset(new (std::nothrow) size_t[kMaxDirectSlots * kern::kMaxRows]);
+            s.ddst_hi.reset(new (std::nothrow) size_t[kMaxDirectSlots * kern::kMaxRows]);
+            if (!s.dsrc || !s.dsrc_n || !s.dsrc_lo || !s.dsrc_hi || !s.ddst || !s.ddst_lo || !s.ddst_hi)
+                return ELECT_EC_ENOMEM;
         }
         try {  // the dispatcher's copies never grow past this (no allocation on its thread)
+            for (auto* v : {&slots_.src_n, &slots_.src_lo, &slots_.src_hi}) v->reserve(kMaxDirectSlots * kern::kMaxCols);
+            for (auto* v : {&slots_.dst_lo, &slots_.dst_hi}) v->reserve(kMaxDirectSlots * kern::kMaxRows);
             slots_.src.reserve(kMaxDirectSlots * kern::kMaxCols);
-            slots_.src_n.reserve(kMaxDirectSlots * kern::kMaxCols);
             slots_.dst.reserve(kMaxDirectSlots * kern::kMaxRows);
         } catch (const std::bad_alloc&) {
             return ELECT_EC_ENOMEM;
@@ -881,7 +1362,7 @@ private:
             if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
             for (uint8_t* h : {s.pin_in, s.pin_out})
                 if (h) (void)hipHostFree(h);
-            for (void* h : {static_cast<void*>(s.pin_lens), static_cast<void*>(s.pin_hash)})
+            for (void* h : {static_cast<void*>(s.pin_lens), static_cast<void*>(s.pin_hash), static_cast<void*>(s.pieces)})
                 if (h) (void)hipHostFree(h);
             for (void* d : {static_cast<void*>(s.d_in), static_cast<void*>(s.d_out), static_cast<void*>(s.d_lens),
                             static_cast<void*>(s.d_hash), static_cast<void*>(s.d_scratch)})
@@ -891,6 +1372,9 @@ private:
             s.pin_in = s.pin_out = s.d_in = s.d_out = nullptr;
             s.pin_lens = s.d_lens = nullptr;
             s.pin_hash = s.d_hash = nullptr;
+            s.pieces = nullptr;
+            s.pieces_dev = nullptr;
+            s.pin_in_dev = s.pin_out_dev = nullptr;
             s.d_scratch = nullptr;
         }
         arena_ = 0;
@@ -932,10 +1416,16 @@ private:
                 const size_t ni = static_cast<size_t>(n) * kern::kMaxCols, no = static_cast<size_t>(n) * kern::kMaxRows;
                 slots_.src.assign(s->dsrc.get(), s->dsrc.get() + ni);
                 slots_.src_n.assign(s->dsrc_n.get(), s->dsrc_n.get() + ni);
+                slots_.src_lo.assign(s->dsrc_lo.get(), s->dsrc_lo.get() + ni);
+                slots_.src_hi.assign(s->dsrc_hi.get(), s->dsrc_hi.get() + ni);
                 slots_.dst.assign(s->ddst.get(), s->ddst.get() + no);
+                slots_.dst_lo.assign(s->ddst_lo.get(), s->ddst_lo.get() + no);
+                slots_.dst_hi.assign(s->ddst_hi.get(), s->ddst_hi.get() + no);
             }
             lock.unlock();
+            const uint64_t t0 = thread_cpu_ns();
             const hipError_t e = issue(*s, shape, n, slots_);
+            g_issue_cpu_ns.fetch_add(thread_cpu_ns() - t0);
             if (e != hipSuccess) (void)hipStreamSynchronize(s->stream);  // no callback was queued
             lock.lock();
             if (e != hipSuccess) finish(s, map_hip(e));
@@ -950,16 +1440,68 @@ private:
         const size_t in_stride = sh.tiles * sh.cols * sh.pitch;  // per slot
         const size_t out_stride = sh.tiles * sh.rows * sh.pitch;
         hipError_t e = hipSuccess;
-        // Direct batches: one DMA per unit, on the slab's one stream (spreading them
-        // over two streams lost 6-8 GiB/s at 16 and 64 callers, profiles/r04/direct_streams_ab.txt).
-        if (sh.direct) {  // every unit straight from its caller's page-locked buffer
-            for (int q = 0; q < n && e == hipSuccess; ++q)
-                for (int j = 0; j < sh.cols && e == hipSuccess; ++j) {
-                    const size_t i = static_cast<size_t>(q) * kern::kMaxCols + j;
-                    if (d.src_n[i])
-                        e = hipMemcpyAsync(s.d_in + q * in_stride + j * sh.pitch, d.src[i], d.src_n[i],
-                                           hipMemcpyHostToDevice, s.stream);
+        // Direct batches: each unit's [lo, hi) straight from its caller's page-locked
+        // memory, the rest (a locked unit's partial end pages) from the arena.
+        // By kernel (the default): one gather launch reads every piece over PCIe
+        // into the device arena, one scatter launch writes the outputs back; the
+        // piece table is written here and read by the kernels where it lies.
+        // By DMA (ELECT_EC_DIRECT_MOVE=dma, round 4's way, pool units only): a
+        // hipMemcpyAsync per piece, all on the slab's one stream (spreading them
+        // over two streams lost 6-8 GiB/s at 16 and 64 callers,
+        // profiles/r04/direct_streams_ab.txt); pieces contiguous on both sides
+        // with the one before share its DMA.
+        const bool by_kernel = direct_by_kernel();
+        size_t gather_n = 0, scatter_n = 0;
+        if (sh.direct && by_kernel) {
+            size_t np = 0;
+            bool overflow = false;
+            auto piece = [&](const uint8_t* from, uint8_t* to, size_t bytes) {
+                for (size_t o = 0; o < bytes; o += kern::kMaxPieceBytes) {
+                    if (np == s.max_pieces) {
+                        overflow = true;
+                        return;
+                    }
+                    s.pieces[np++] = kern::CopyPiece{from + o, to + o,
+                                                     static_cast<uint32_t>(std::min<size_t>(kern::kMaxPieceBytes, bytes - o)), 0};
                 }
+            };
+            for (int q = 0; q < n; ++q)
+                for (int j = 0; j < sh.cols; ++j) {
+                    const size_t i = static_cast<size_t>(q) * kern::kMaxCols + j;
+                    const size_t nb = d.src_n[i], lo = d.src_lo[i], hi = d.src_hi[i];
+                    uint8_t* const dev = s.d_in + q * in_stride + j * sh.pitch;
+                    const uint8_t* const pin = s.pin_in_dev + q * in_stride + j * sh.pitch;
+                    piece(pin, dev, lo);
+                    piece(d.src[i] + lo, dev + lo, hi - lo);
+                    piece(pin + hi, dev + hi, nb - hi);
+                }
+            gather_n = np;
+            for (int q = 0; q < n; ++q)
+                for (int r = 0; r < sh.rows; ++r) {
+                    const size_t i = static_cast<size_t>(q) * kern::kMaxRows + r;
+                    const size_t lo = d.dst_lo[i], hi = d.dst_hi[i];
+                    const uint8_t* const dev = s.d_out + q * out_stride + r * sh.pitch;
+                    uint8_t* const pin = s.pin_out_dev + q * out_stride + r * sh.pitch;
+                    piece(dev, pin, lo);
+                    piece(dev + lo, d.dst[i] + lo, hi - lo);
+                    piece(dev + hi, pin + hi, sh.len - hi);
+                }
+            scatter_n = np - gather_n;
+            e = overflow ? hipErrorInvalidValue
+                         : kern::launch_copy_pieces(s.pieces_dev, static_cast<uint32_t>(gather_n), s.stream);
+        } else if (sh.direct) {
+            Dma dma(hipMemcpyHostToDevice, s.stream);
+            for (int q = 0; q < n; ++q)
+                for (int j = 0; j < sh.cols; ++j) {
+                    const size_t i = static_cast<size_t>(q) * kern::kMaxCols + j;
+                    const size_t nb = d.src_n[i], lo = d.src_lo[i], hi = d.src_hi[i];
+                    uint8_t* const dev = s.d_in + q * in_stride + j * sh.pitch;
+                    const uint8_t* const pin = s.pin_in + q * in_stride + j * sh.pitch;
+                    dma.add(dev, pin, lo);
+                    dma.add(dev + lo, d.src[i] + lo, hi - lo);
+                    dma.add(dev + hi, pin + hi, nb - hi);
+                }
+            e = dma.flush();
         } else {
             e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
         }
@@ -996,11 +1538,21 @@ private:
             }
             e = kern::launch_apply(p, s.stream);
         }
-        if (e == hipSuccess && sh.direct) {
-            for (int q = 0; q < n && e == hipSuccess; ++q)
-                for (int r = 0; r < sh.rows && e == hipSuccess; ++r)
-                    e = hipMemcpyAsync(d.dst[static_cast<size_t>(q) * kern::kMaxRows + r], s.d_out + q * out_stride + r * sh.pitch,
-                                       sh.len, hipMemcpyDeviceToHost, s.stream);
+        if (e == hipSuccess && sh.direct && by_kernel) {
+            e = kern::launch_copy_pieces(s.pieces_dev + gather_n, static_cast<uint32_t>(scatter_n), s.stream);
+        } else if (e == hipSuccess && sh.direct) {
+            Dma dma(hipMemcpyDeviceToHost, s.stream);
+            for (int q = 0; q < n; ++q)
+                for (int r = 0; r < sh.rows; ++r) {
+                    const size_t i = static_cast<size_t>(q) * kern::kMaxRows + r;
+                    const size_t lo = d.dst_lo[i], hi = d.dst_hi[i];
+                    const uint8_t* const dev = s.d_out + q * out_stride + r * sh.pitch;
+                    uint8_t* const pin = s.pin_out + q * out_stride + r * sh.pitch;
+                    dma.add(pin, dev, lo);
+                    dma.add(d.dst[i] + lo, dev + lo, hi - lo);
+                    dma.add(pin + hi, dev + hi, sh.len - hi);
+                }
+            e = dma.flush();
         } else if (e == hipSuccess) {
             e = hipMemcpyAsync(s.pin_out, s.d_out, n * out_stride, hipMemcpyDeviceToHost, s.stream);
         }
@@ -1010,6 +1562,38 @@ private:
         if (e == hipSuccess) e = hipLaunchHostFunc(s.stream, &Batcher::on_done, &s);
         return e;
     }
+
+    // hipMemcpyAsync calls of one direction, a piece contiguous on both sides with
+    // the previous one extending it.  The first error stops the issue.
+    struct Dma {
+        hipMemcpyKind kind;
+        hipStream_t stream;
+        uint8_t* dst = nullptr;
+        const uint8_t* src = nullptr;
+        size_t n = 0;
+        hipError_t e = hipSuccess;
+        Dma(hipMemcpyKind k, hipStream_t s) : kind(k), stream(s) {}
+        void add(void* to, const void* from, size_t bytes)
+        {
+            if (!bytes || e != hipSuccess) return;
+            auto* t = static_cast<uint8_t*>(to);
+            auto* f = static_cast<const uint8_t*>(from);
+            if (n && t == dst + n && f == src + n) {
+                n += bytes;
+                return;
+            }
+            flush();
+            dst = t;
+            src = f;
+            n = bytes;
+        }
+        hipError_t flush()
+        {
+            if (n && e == hipSuccess) e = hipMemcpyAsync(dst, src, n, kind, stream);
+            n = 0;
+            return e;
+        }
+    };
 
     static void on_done(void* arg)  // HIP host-function callback: no HIP calls in here
     {
@@ -1103,20 +1687,8 @@ struct ZeroCopy {
         return m == 2 || (len >= kMinBytes && in_flight <= kMaxInFlight && alone);
     }
 
-    // Bytes of input j the kernels may touch: a padded unit's content rounded up
-    // to the 16-byte segment, never past the unit.  The padded vector kernel
-    // loads the whole segment that holds a content end (rs_impl.hpp,
-    // gf_apply_x16<PAD>) and masks it: up to 15 bytes past lens[j], which on a
-    // caller pointer off 16-byte alignment can cross into a page registered for
-    // nothing.  So those bytes are registered too.
-    static size_t input_span(const HostOp& op, int j, size_t len)
-    {
-        if (!op.lens) return len;
-        return std::min(len, (op.lens[j] + 15) & ~size_t{15});
-    }
-
     // Page-aligned, merged [begin, end) intervals covering every byte the
-    // call's kernels touch.
+    // call's kernels touch (inputs: input_span).
     static std::vector<std::pair<uintptr_t, uintptr_t>> ranges(const HostOp& op, size_t len)
     {
         constexpr uintptr_t kPage = 4096;
@@ -1168,12 +1740,13 @@ struct ZeroCopy {
             return kFallback;
         }
         hipStream_t stream = ts.stream[dev];
+        // through the registry: a range sharing a page with any live registration
+        // (another thread's call) is refused, and the call falls back to the staged path
         const auto rs = pinned ? std::vector<std::pair<uintptr_t, uintptr_t>>{} : ranges(op, len);
+        Registrar& reg = Registrar::get();
         size_t locked = 0;
         for (; locked < rs.size(); ++locked)
-            if (hipHostRegister(reinterpret_cast<void*>(rs[locked].first), rs[locked].second - rs[locked].first,
-                                hipHostRegisterMapped) != hipSuccess)
-                break;
+            if (!reg.acquire(rs[locked].first, rs[locked].second, Registrar::kHipRegister)) break;
         int rc = kFallback;
         if (locked == rs.size()) {
             ApplyParams p;
@@ -1211,8 +1784,7 @@ struct ZeroCopy {
                 rc = e == hipErrorInvalidValue ? kFallback : map_hip(e);
             }
         }
-        for (size_t i = 0; i < locked; ++i) (void)hipHostUnregister(reinterpret_cast<void*>(rs[i].first));
-        (void)hipGetLastError();  // a failed registration is not this thread's next call's error
+        for (size_t i = 0; i < locked; ++i) reg.release(rs[i].first);  // (the stream is synchronised above)
         return rc;
     }
 };
@@ -1238,8 +1810,11 @@ bool lone_caller(int dev)
     return now - g_other_caller_ns[dev].load() > kAloneNs;
 }
 // elect_ec_host_path_stats: zero-copy calls, zero-copy fallbacks, batched (staged), per-thread
-// engine, batched direct (page-locked caller buffers, no staging copies).
-constexpr int kStats = 5;
+// engine, batched direct (page-locked caller buffers, no staging copies), batched direct on
+// units registered for the call (ELECT_EC_REGISTER=1), registration attempts that fell back
+// to staging (no free slot, or a range refused), failed unregistrations (entry 7 is read from
+// g_unregister_failures), CPU ns registering / unregistering / issuing batches (8-10).
+constexpr int kStats = 11;
 std::atomic<uint64_t> g_stats[kStats];
 
 }  // namespace
@@ -1286,8 +1861,29 @@ int run_host(const HostOp& op, size_t len)
         }
         if (batch_config().enabled.load() == 1) {
             Batcher* b = batcher(dev);
-            rc = b ? b->submit(op, len, direct) : ELECT_EC_ENOMEM;
-            if (rc != Batcher::kFallback) g_stats[direct ? 4 : 2].fetch_add(1);
+            DirectPlan plan;
+            bool registered = false;
+            if (direct) {  // pool units: all of each straight from / to the pool buffer
+                PinnedPool& pool = PinnedPool::get();
+                plan.direct = true;
+                for (int j = 0; j < op.cols; ++j) {
+                    plan.in_hi[j] = op.lens ? op.lens[j] : len;
+                    plan.in_dev[j] = plan.in_hi[j] ? pool.device_addr(op.in[j]) : 0;
+                }
+                for (int r = 0; r < op.rows; ++r) {
+                    plan.out_hi[r] = len;
+                    plan.out_dev[r] = pool.device_addr(op.out[r]);
+                }
+            } else if (b && RegisterPath::mode() == 1 && len >= RegisterPath::kMinBytes) {
+                registered = RegisterPath::plan(op, len, dev, plan);
+                if (!registered) g_stats[6].fetch_add(1);
+            }
+            struct Release {  // the registrations outlive the call's batch, not the call
+                DirectPlan& p;
+                ~Release() { RegisterPath::release(p); }
+            } release{plan};
+            rc = b ? b->submit(op, len, &plan) : ELECT_EC_ENOMEM;
+            if (rc != Batcher::kFallback) g_stats[registered ? 5 : direct ? 4 : 2].fetch_add(1);
         }
         if (rc == Batcher::kFallback) {
             if (!t_engines[dev]) t_engines[dev].reset(new (std::nothrow) HostEngine(dev));
@@ -1329,6 +1925,10 @@ int host_path_stats(uint64_t* out, int n)
 {
     if (n < 0 || (n > 0 && !out)) return ELECT_EC_EINVAL;
     const int w = n < kStats ? n : kStats;
+    g_stats[7].store(g_unregister_failures.load());
+    g_stats[8].store(g_register_cpu_ns.load());
+    g_stats[9].store(g_unregister_cpu_ns.load());
+    g_stats[10].store(g_issue_cpu_ns.load());
     for (int i = 0; i < w; ++i) out[i] = g_stats[i].load();
     return w;
 }

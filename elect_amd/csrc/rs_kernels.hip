@@ -465,6 +465,87 @@ hipError_t hbm_probe(int kind, const void* src, void* dst, size_t bytes, int blo
     return hipGetLastError();
 }
 
+// Host <-> device gathers and scatters of the host path's direct batches
+// (host_path.cpp): one block per piece of at most kMaxPieceBytes, 16-byte
+// vector loads and stores at any byte offset (unaligned_vector_ok; the byte
+// loop otherwise), non-temporal both ways (every byte is moved once).  One of
+// the two ends is page-locked host memory, read or written over PCIe through
+// its device address (a locked caller unit or an elect_ec_host_alloc /
+// arena buffer, mapped at its host address): round 5 measured such kernels
+// at 49 GB/s reading and 51 GB/s writing host memory
+// (profiles/r05/register_overlap.txt, part 4), with no DMA engine and no
+// runtime transfer call per unit.
+template <bool VEC, bool NT, int U>
+__global__ __launch_bounds__(kBlock) void copy_pieces_kernel(const CopyPiece* __restrict__ pieces, uint32_t n)
+{
+  for (uint32_t pi = blockIdx.x; pi < n; pi += gridDim.x) {
+    const CopyPiece pc = pieces[pi];
+    const uint32_t vecs = VEC ? pc.n / 16 : 0;
+    uint32_t v = threadIdx.x;
+    // U loads in flight per lane before their stores
+    for (; v + (U - 1) * kBlock < vecs; v += U * kBlock) {
+        uint4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint8_t* s = pc.src + (v + u * kBlock) * 16;
+            if constexpr (NT)
+                x[u] = load_nt(s);
+            else
+                __builtin_memcpy(&x[u], s, 16);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            uint8_t* d = pc.dst + (v + u * kBlock) * 16;
+            if constexpr (NT)
+                store_nt(d, x[u]);
+            else
+                __builtin_memcpy(d, &x[u], 16);
+        }
+    }
+    for (; v < vecs; v += kBlock) {
+        uint4 x;
+        __builtin_memcpy(&x, pc.src + v * 16, 16);
+        __builtin_memcpy(pc.dst + v * 16, &x, 16);
+    }
+    for (uint32_t b = vecs * 16 + threadIdx.x; b < pc.n; b += kBlock) pc.dst[b] = pc.src[b];
+  }
+}
+
+hipError_t launch_copy_pieces(const CopyPiece* pieces, uint32_t n, hipStream_t stream)
+{
+    (void)hipGetLastError();
+    if (n == 0) return hipSuccess;
+    if (n > 0x7FFFFFFFu) return hipErrorInvalidValue;
+    // ELECT_EC_COPY_VARIANT (A/B): 0 plain loads/stores, 4 in flight (default); 1 non-temporal, 4 in
+    // flight; 2 plain, one at a time; 3 non-temporal, one at a time
+    static const int variant = [] {
+        const char* e = std::getenv("ELECT_EC_COPY_VARIANT");
+        return e ? std::atoi(e) : 0;
+    }();
+    // Few blocks (ELECT_EC_COPY_BLOCKS, default 128, half a block per CU): the copies wait on
+    // PCIe, and a full-chip grid of them held the coding launches of other batches off the CUs
+    // (round 5 kernel trace: a 66 us encode stretched to 3.8-5.3 ms beside the copies).  64
+    // callers on ELECT's codeLength, pageable units (profiles/r05/hostpath_copy_ab.txt): 64 /
+    // 128 / 256 / 512 / 2048 blocks 44.7 / 47.9 / 44.4 / 39.2 / 38.1 GiB/s.
+    static const uint32_t cap = [] {
+        const char* e = std::getenv("ELECT_EC_COPY_BLOCKS");
+        const int v = e ? std::atoi(e) : 128;
+        return static_cast<uint32_t>(v > 0 ? v : 128);
+    }();
+    const uint32_t grid = std::min(n, cap);
+    if (!unaligned_vector_ok())
+        hipLaunchKernelGGL((copy_pieces_kernel<false, false, 1>), dim3(grid), dim3(kBlock), 0, stream, pieces, n);
+    else if (variant == 1)
+        hipLaunchKernelGGL((copy_pieces_kernel<true, true, 4>), dim3(grid), dim3(kBlock), 0, stream, pieces, n);
+    else if (variant == 2)
+        hipLaunchKernelGGL((copy_pieces_kernel<true, false, 1>), dim3(grid), dim3(kBlock), 0, stream, pieces, n);
+    else if (variant == 3)
+        hipLaunchKernelGGL((copy_pieces_kernel<true, true, 1>), dim3(grid), dim3(kBlock), 0, stream, pieces, n);
+    else
+        hipLaunchKernelGGL((copy_pieces_kernel<true, false, 4>), dim3(grid), dim3(kBlock), 0, stream, pieces, n);
+    return hipGetLastError();
+}
+
 bool apply_is_aligned(const ApplyParams& p)
 {
     for (int j = 0; j < p.cols; ++j)

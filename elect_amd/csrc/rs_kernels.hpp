@@ -124,6 +124,19 @@ hipError_t launch_apply_many(const ApplyParams* ps, int n, hipStream_t stream);
 constexpr size_t hash_scratch_need(uint64_t segments) { return (segments / 64 + 1) * kFastRows * 2; }
 hipError_t launch_update(const UpdateParams& p, hipStream_t stream);
 
+// One piece of a gather / scatter between host and device memory (host path,
+// direct batches): n bytes from src to dst, both device-accessible addresses.
+struct CopyPiece {
+    const uint8_t* src;
+    uint8_t* dst;
+    uint32_t n;
+    uint32_t pad;
+};
+constexpr uint32_t kMaxPieceBytes = 1u << 16;  // callers split longer ranges
+
+// Copies every piece of the device array `pieces` (one block each).
+hipError_t launch_copy_pieces(const CopyPiece* pieces, uint32_t n, hipStream_t stream);
+
 // True when every column start is 16-byte aligned for every stripe.
 bool apply_is_aligned(const ApplyParams& p);
 

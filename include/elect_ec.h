@@ -128,8 +128,16 @@ int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes);
  * out[1] zero-copy attempts that fell back (registration refused), out[2]
  * calls coded through the cross-thread batcher with staging copies, out[3]
  * calls coded by the per-thread staging engine, out[4] calls coded through the
- * batcher by DMA straight from and to elect_ec_host_alloc buffers.  Writes
- * min(n, 5) entries; returns the count. */
+ * batcher by DMA straight from and to elect_ec_host_alloc buffers, out[5] calls
+ * coded through the batcher by DMA straight from and to the caller's own
+ * pageable units, page-locked for the call (ELECT_EC_REGISTER=1: each unit's
+ * interior pages; its partial end pages are staged), out[6] such attempts that
+ * took the staged path instead (no free registration slot, ELECT_EC_REGISTER_SLOTS,
+ * or a range refused because it shares a page with a live registration of
+ * another extent), out[7] hipHostUnregister failures (0 unless the runtime's
+ * registrations were disturbed by another party), out[8..10] CPU time in ns
+ * spent registering, unregistering, and issuing batches in the dispatcher
+ * threads.  Writes min(n, 11) entries; returns the count. */
 int elect_ec_host_path_stats(uint64_t* out, int n);
 
 /* Page-locked host memory for the units of host-memory calls.  ELECT allocates

@@ -22,7 +22,8 @@ def _zf(x, n):
 
 def _pinned(n, fill=None, keep=None):
     hb = _lib.HostBuffer(n)
-    assert _lib.host_pinned(hb.addr, n), "elect_ec_host_alloc on a GPU box must be page-locked"
+    assert _lib.host_pinned(hb.addr, n), ("elect_ec_host_alloc on a GPU box must be page-locked",
+                                          hex(hb.addr), n, _lib.host_pinned(hb.addr, 1))
     if fill is not None:
         hb.array[:] = fill
     if keep is not None:
@@ -79,7 +80,9 @@ def test_direct_entry_points_match_oracle(dev, oracle, L):
 
 
 def test_direct_needs_every_unit_in_the_pool(dev, oracle):
-    """One output in ordinary memory: the call is staged, and right."""
+    """One output in ordinary memory: the call is not a pool-direct call; it is
+    coded with that output's interior pages locked for the call (or staged), and
+    right."""
     from elect_amd.coder import RSCoder
     L = 4404020
     rng = np.random.default_rng(5)
@@ -90,7 +93,7 @@ def test_direct_needs_every_unit_in_the_pool(dev, oracle):
     RSCoder(K, M).encode_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L)
     assert all(np.array_equal(a, b) for a, b in zip(p, oracle.Encoder(K, M).encode(list(d))))
     dl = _delta(st)
-    assert dl["direct"] == 0 and dl["batched"] + dl["zero_copy"] + dl["per_thread"] == 1, dl
+    assert dl["direct"] == 0 and dl["batched"] + dl["registered"] + dl["zero_copy"] + dl["per_thread"] == 1, dl
     for hb in keep:
         hb.close()
 

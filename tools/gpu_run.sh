@@ -127,6 +127,30 @@ for step in "$@"; do
         SANITIZER=tsan run tsan_stress 600 bash tools/sanitize/run.sh run ${TSAN_T:-8} ${TSAN_N:-4} || exit $? ;;
     asan)  # the host stress under ASan + UBSan
         run asan_stress 600 bash tools/sanitize/run.sh run || exit $? ;;
+    hostreg)  # per-call registration of pageable units (ELECT_EC_REGISTER=1) vs staged, ELECT's codeLength, interleaved
+        for i in 1 2; do for rg in ${REG_MODES:-0 1}; do for T in ${T_LIST:-64 16}; do for sl in ${REG_SLOTS:-2}; do
+            [ $rg = 0 ] && [ $sl != ${REG_SLOTS%% *} ] && continue  # staged: once per (T, rep)
+            ELECT_EC_REGISTER_SLOTS=$sl run "bench_hostpath_reg${rg}_s${sl}_T${T}_$i" 300 python bench.py --config hostpath \
+                --threads $T --host-register $rg --host-seconds 2 --steps 8 --host-op ${HOST_OP:-encode} || exit $?
+        done; done; done; done ;;
+    hostpinned)  # page-locked pool callers: gather/scatter kernels vs round 4's per-unit DMAs, interleaved
+        for i in 1 2; do for mv in kernel dma; do for T in ${T_LIST:-64 16}; do
+            ELECT_EC_DIRECT_MOVE=$mv run "bench_hostpath_pinned_${mv}_T${T}_$i" 300 python bench.py --config hostpath \
+                --threads $T --host-alloc pinned --host-seconds 2 --steps 8 --host-op ${HOST_OP:-encode} || exit $?
+        done; done; done ;;
+    hostcopyvar)  # the direct batches' gather/scatter kernel variants (ELECT_EC_COPY_VARIANT), pinned and pageable
+        for i in 1 2; do for v in ${VARIANTS:-0 1 2 3}; do for cb in ${COPY_BLOCKS:-512}; do for alloc in ${ALLOCS:-pinned pageable}; do
+            ELECT_EC_COPY_VARIANT=$v ELECT_EC_COPY_BLOCKS=$cb run "bench_hostpath_cv${v}_cb${cb}_${alloc}_T64_$i" 300 python bench.py --config hostpath \
+                --threads 64 --host-alloc $alloc --host-seconds 2 --steps 8 || exit $?
+        done; done; done; done ;;
+    hostblock)  # the dispatcher's wait on the previous batch: polled (default) vs blocking event, interleaved
+        for i in 1 2; do for b in 0 1; do for alloc in ${ALLOCS:-pageable pinned}; do
+            ELECT_EC_DISPATCH_BLOCKING=$b run "bench_hostpath_blk${b}_${alloc}_T64_$i" 300 python bench.py --config hostpath \
+                --threads 64 --host-alloc $alloc --host-seconds 2 --steps 8 || exit $?
+        done; done; done ;;
+    hostprof)  # kernel trace of the pageable host path at 64 callers (gather / code / scatter durations)
+        run hostprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/hostprof_$TAG -o run \
+            -- python3 bench.py --config hostpath --threads 64 --host-seconds 2 --steps 8 || exit $? ;;
     hostsweep) run hostsweep 600 python tools/tune/host_sweep.py || exit $? ;;
     copysizes) run copysizes 600 python tools/tune/host_sweep.py copysizes || exit $? ;;
     staged)

@@ -34,7 +34,7 @@ build)
         [ $((k % 8)) -eq 0 ] && wait
     done
     wait
-    $H --offload-arch=gfx950 -shared -fPIC $SAN -o $OUT/libelect_ec_san.so $objs
+    $H --offload-arch=gfx950 -shared -fPIC $SAN -o $OUT/libelect_ec_san.so $objs -L/opt/rocm/lib -lhsa-runtime64
     $H --offload-arch=gfx950 -O1 -g -std=c++17 -I include $SAN -x hip tools/sanitize/host_stress.cpp -o $OUT/host_stress \
         -L $OUT -lelect_ec_san -Wl,-rpath,'$ORIGIN' -pthread
     rm -f $OUT/*.o
