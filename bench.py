@@ -532,6 +532,22 @@ def decode_sweep(coder, stripe, stream, reps=5):
     return res
 
 
+def parity_rows_verified(coder, stripe, decode=None) -> bool:
+    """Every parity row the encode wrote, checked through the product: erase data
+    units 0..m-1 and rebuild them from the other data units plus ALL m parity
+    units (EC/erasure_coder.c:90-91: every one of the m rows is an output).  The
+    timed decodes read parity unit k only (survivors 1..k), so a defect confined
+    to another parity row would otherwise leave `verified` true.  Outside the
+    timed region.  decode: the decode_batch to use (a CPU test injects its own)."""
+    if decode is None:
+        from elect_amd.batch import decode_batch as decode
+    k, m = coder.k, coder.m
+    B, L = stripe.shape[0], stripe.shape[2]
+    out = torch.empty((B, m, L), dtype=stripe.dtype, device=stripe.device)
+    decode(coder, stripe, list(range(m, k + m)), list(range(m)), out, inputs_by_unit=True)
+    return bool(torch.equal(out, stripe[:, :m]))
+
+
 def size_sweep(args, world, rank, dev, coder, sizes=(1024, 1 << 20)):
     """The north star's other chunk sizes (1 KiB and 1 MiB next to the headline's
     64 KiB), each timed exactly like the headline after it: the same step
@@ -570,7 +586,8 @@ def size_sweep(args, world, rank, dev, coder, sizes=(1024, 1 << 20)):
             "layout": LAYOUT_NAMES[layout_for(args, L)],
             "encode_frac": round(B * (k + m) * L / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "decode_frac": round(B * (k + 1) * L / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "verified": all(bool(torch.equal(out[:, 0], st[:, 0])) for st, out in sets)}
+            "verified": all(bool(torch.equal(out[:, 0], st[:, 0])) for st, out in sets) and
+                        all(parity_rows_verified(coder, st) for st, _ in sets)}
         del sets
     return res
 
@@ -938,7 +955,7 @@ def config_rs12(args, world, rank, dev):
         e1.record()
         enc_ev.append((e0, e1))
     torch.cuda.synchronize()
-    ok = ok and torch.equal(par, st[:, k:])
+    ok = ok and torch.equal(par, st[:, k:]) and parity_rows_verified(coder, st)  # parity rows 0..3 all read
     enc_ms = sorted(a.elapsed_time(b) for a, b in enc_ev)[len(enc_ev) // 2]
     enc_gbs = B * (k + m) * L / (enc_ms * 1e-3) / 1e9
     name = {1: "single", 2: "two", 3: "three", 4: "four"}[e]
@@ -1092,7 +1109,11 @@ def config_hostpath(args, world, rank, dev):
 
 
 HOSTPATH_CALLERS = 64  # ELECT's concurrent_ec (conf/elect.yaml:598)
-HOSTPATH_CHILD_TIMEOUT_S = 420
+# The children of hostpath_all_devices share one deadline, well inside the 10-minute gloo
+# timeout the other ranks wait under at the barrier (elect_amd/dist.py): a slow or hung child
+# yields a verified=false record, never a dead job.
+HOSTPATH_TOTAL_TIMEOUT_S = 480
+HOSTPATH_CHILD_TIMEOUT_S = 280
 
 
 def hostpath_child_cmd(ndev: int, alloc: str = "pageable") -> list:
@@ -1130,14 +1151,17 @@ def hostpath_all_devices(args, world, rank, child=None):
     if rank == 0:
         ndev = world if child is not None else min(world, torch.cuda.device_count())
         runs = [("pageable", child)] if child is not None else [("pageable", None), ("pinned", None)]
+        deadline = time.monotonic() + HOSTPATH_TOTAL_TIMEOUT_S
         for alloc, cmd_override in runs:
             cmd = cmd_override if cmd_override is not None else hostpath_child_cmd(ndev, alloc)
-            try:  # (well inside the gloo group's 10-minute timeout the other ranks wait under)
-                r = subprocess.run(cmd, capture_output=True, text=True, env=child_env(),
-                                   timeout=HOSTPATH_CHILD_TIMEOUT_S)
+            limit = min(HOSTPATH_CHILD_TIMEOUT_S, deadline - time.monotonic())
+            try:
+                if limit <= 0:
+                    raise subprocess.TimeoutExpired(cmd, 0)
+                r = subprocess.run(cmd, capture_output=True, text=True, env=child_env(), timeout=limit)
             except subprocess.TimeoutExpired as e:
                 r = subprocess.CompletedProcess(cmd, -9, (e.stdout or b"").decode(errors="replace") if isinstance(
-                    e.stdout, bytes) else (e.stdout or ""), f"timed out after {HOSTPATH_CHILD_TIMEOUT_S} s")
+                    e.stdout, bytes) else (e.stdout or ""), f"timed out after {max(0.0, limit):.0f} s")
             line = next((x for x in reversed(r.stdout.splitlines()) if x.startswith("{")), None)
             if r.returncode != 0 or line is None:
                 rec = {"verified": False, "devices": ndev, "error": f"rc={r.returncode}: {(r.stderr or r.stdout)[-400:]}"}
@@ -1607,6 +1631,9 @@ def main():
         ok = bool(torch.equal(stripe[:, 0], orig0))
     else:
         ok = all(bool(torch.equal(r[:, 0], st[:, 0])) for st, r in sets)
+    # every parity row of every batch (the timed decodes read parity unit k only)
+    parity_ok = all(parity_rows_verified(coder, st) for st, _ in sets)
+    ok = ok and parity_ok
 
     data_bytes_per_rank_step = 2 * B * k * L  # encode k*L + decode k*L survivors, per stripe
     value = world * args.steps * data_bytes_per_rank_step / elapsed / GIB
@@ -1666,6 +1693,7 @@ def main():
                                 "data_GiB/s": round(B * k * L / (dec_ms * 1e-3) / GIB, 1)},
         },
         "verified": ok,
+        "verified_parity_rows": parity_ok,
     }
     if per_step:
         out["per_step_ms"] = per_step

@@ -249,13 +249,17 @@ def host_pinned(addr: int, nbytes: int) -> bool:
 
 class HostBuffer:
     """An elect_ec_host_alloc buffer as a numpy uint8 array (what a JVM would wrap in a
-    direct ByteBuffer); freed on close() or garbage collection."""
+    direct ByteBuffer); freed on close(), or by garbage collection once neither the
+    HostBuffer nor its .array is referenced (the array keeps its owner alive, so a
+    kept array never outlives its memory: ADVICE r4)."""
 
     def __init__(self, nbytes: int):
         import numpy as np
         self.addr = host_alloc(nbytes)
         self.nbytes = nbytes
-        self.array = np.ctypeslib.as_array((ctypes.c_ubyte * nbytes).from_address(self.addr))
+        buf = (ctypes.c_ubyte * nbytes).from_address(self.addr)
+        buf._owner = self  # array -> buf -> self: the memory stays allocated while the array lives
+        self.array = np.ctypeslib.as_array(buf)
 
     def close(self) -> None:
         if self.addr:

@@ -1159,7 +1159,9 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
             if (!a.hashes) {
                 bool launched = false;
                 if constexpr (kPolicy.plain_lds_dma > 0) {  // one-wave launches load through LDS
-                    if (sh.block == 64 && (kPolicy.plain_lds_dma > 1 || 2 * R < K)) {
+                    // (16-byte aligned columns only: unaligned_vector_ok() vouches for global_load_dwordx4
+                    // at any offset, not for the LDS-DMA load)
+                    if (sh.block == 64 && p.aligned16 && (kPolicy.plain_lds_dma > 1 || 2 * R < K)) {
                         const size_t lds_d = cap_lds(sh, kCoefs, K * 1024);
                         if (scalar_base && K >= kPolicy.scalar_base_min_cols)
                             hipLaunchKernelGGL((gf_apply_x16u<K, R, false, true>), grid, dim3(sh.block), lds_d, stream, a);

@@ -13,11 +13,12 @@ namespace {
 
 // Hash-partial scratch when the caller brings none (the device-resident API):
 // one buffer per (device, stream), reused only in that stream's order.  It is
-// handed to another stream (16 entries per device, least recently used first)
+// handed to another stream (64 entries per device, least recently used first)
 // only after a device-wide synchronize, and grown only after its own stream's
 // synchronize, so a hashed call records nothing on the stream: a completion
 // marker behind every call held the next launch back ~1.5 us (round 4,
-// profiles/r04/event_cost.txt), and streams beyond 16 are rare.
+// profiles/r04/event_cost.txt), and streams beyond 64 are rare (16 entries made
+// the device-wide synchronize of a handoff routine for 17+ concurrently launching streams).
 // Stream-ordered allocation (hipMallocAsync / hipFreeAsync, default or private
 // pool) corrupted partials when many threads launched on their own streams:
 // freed blocks were handed out again while a reduce still read them
@@ -36,7 +37,7 @@ struct ScratchEntry {
 struct ScratchCache {
     std::mutex mu;
     uint64_t tick = 0;
-    ScratchEntry e[16];
+    ScratchEntry e[64];
 };
 
 ScratchCache g_scratch[64];

@@ -120,9 +120,14 @@ def test_hostpath_child_timeout_is_a_record_not_a_crash():
     rank 0 (the line still prints, and fails), not an exception that would leave
     the other ranks waiting at the barrier; the limit sits inside the gloo timeout."""
     mod = _bench_module()
-    assert mod.HOSTPATH_CHILD_TIMEOUT_S < 10 * 60
+    # every child of the run together stays inside the 10-minute gloo timeout (ADVICE r4)
+    assert mod.HOSTPATH_TOTAL_TIMEOUT_S < 10 * 60 and mod.HOSTPATH_CHILD_TIMEOUT_S <= mod.HOSTPATH_TOTAL_TIMEOUT_S
     mod.HOSTPATH_CHILD_TIMEOUT_S = 1
     res = mod.hostpath_all_devices(None, 1, 0, child=[sys.executable, "-c", "import time; time.sleep(30)"])
+    assert res["verified"] is False and "timed out" in res["error"], res
+    # a spent shared deadline: the next child is not started at all
+    mod.HOSTPATH_CHILD_TIMEOUT_S, mod.HOSTPATH_TOTAL_TIMEOUT_S = 280, 0
+    res = mod.hostpath_all_devices(None, 1, 0, child=[sys.executable, "-c", "print('{}')"])
     assert res["verified"] is False and "timed out" in res["error"], res
 
 
@@ -141,3 +146,47 @@ def test_metric_names_the_chunk():
     mod = _bench_module()
     assert mod.chunk_name(65536) == "64 KiB" and mod.chunk_name(1 << 20) == "1 MiB"
     assert mod.chunk_name(1024) == "1 KiB" and mod.chunk_name(4404020) == "4404020 B"
+
+
+def test_parity_rows_check_sees_every_row():
+    """bench.py's verified flag covers every parity row: the timed
+    decode (erase 0 from survivors 1..k) never reads parity row 1 of RS(6,4), so a
+    corrupted row 1 passes it; parity_rows_verified rebuilds data 0..m-1 from the
+    other data and ALL parity units and catches it.  A fake decode_batch over CPU
+    tensors, built on the oracle (test infrastructure), stands in for the GPU."""
+    import numpy as np
+    import torch
+    from oracle import ec_oracle as orc
+    mod = _bench_module()
+    k, m, B, L = 4, 2, 3, 96
+
+    class Coder:
+        pass
+    coder = Coder()
+    coder.k, coder.m = k, m
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    par = np.stack([np.stack(orc.Encoder(k, m).encode(list(data[b]))) for b in range(B)])
+    st = torch.from_numpy(np.concatenate([data, par], 1))
+
+    def fake_decode(coder, stripe, surv, erased, out, inputs_by_unit=False):
+        assert inputs_by_unit
+        s = stripe.numpy()
+        for b in range(s.shape[0]):
+            got = orc.decode(k, m, [s[b, u] for u in surv], surv, erased)[1]
+            for i, g in enumerate(got):
+                out[b, i] = torch.from_numpy(np.asarray(g))
+
+    def timed_check(stripe):  # what the timed region's decode verifies
+        out = torch.empty((B, 1, L), dtype=torch.uint8)
+        fake_decode(coder, stripe, list(range(1, k + 1)), [0], out, inputs_by_unit=True)
+        return bool(torch.equal(out[:, 0], stripe[:, 0]))
+
+    assert mod.parity_rows_verified(coder, st, fake_decode) and timed_check(st)
+    bad = st.clone()
+    bad[1, k + 1, 7] ^= 0x40  # parity row 1 of stripe 1
+    assert timed_check(bad)  # the timed decode alone cannot see it
+    assert not mod.parity_rows_verified(coder, bad, fake_decode)
+    bad = st.clone()
+    bad[2, k, 0] ^= 1  # parity row 0
+    assert not mod.parity_rows_verified(coder, bad, fake_decode)

@@ -268,3 +268,11 @@ def test_host_alloc_pool_semantics():
     assert _lib.lib.elect_ec_host_free(None) == 0
     p = ctypes.c_void_p()
     assert _lib.lib.elect_ec_host_alloc(0, ctypes.byref(p)) == _lib.EINVAL and not p.value
+    # a kept .array keeps its buffer allocated after the HostBuffer itself is dropped
+    import gc
+    arr = _lib.HostBuffer(4096).array
+    gc.collect()
+    arr[:] = 7
+    owner = arr.base.obj._owner if hasattr(arr.base, "obj") else None
+    assert owner is not None and owner.addr and _lib.lib.elect_ec_host_free(owner.addr) == 0
+    owner.addr = 0  # freed here by hand; its close() is then a no-op

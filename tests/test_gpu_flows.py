@@ -384,13 +384,13 @@ def test_device_lengths_above_chunk_count_as_full(dev, oracle):
         assert torch.equal(out[:, 0], d_data[:, 0])  # unit 0's lengths are all above L: full
 
 
-@pytest.mark.parametrize("threads", [12, 24])
+@pytest.mark.parametrize("threads", [12, 24, 80])
 def test_concurrent_streams_hashed_device_api(dev, oracle, threads):
     """Many threads, each launching hashed encodes on its own stream (the device API
     leases a per-stream scratch for the hash partials).  Stream-ordered pool scratch
     (hipMallocAsync / hipFreeAsync) corrupted partials in exactly this pattern
-    (tools/sanitize/host_stress); every hash must still match the JDK loop.  With 24
-    streams the 16 cached buffers change hands (a device-wide synchronize first)."""
+    (tools/sanitize/host_stress); every hash must still match the JDK loop.  With 80
+    streams the 64 cached buffers change hands (a device-wide synchronize first)."""
     import threading
     from elect_amd.batch import encode_batch_ex
     from elect_amd.coder import RSCoder
