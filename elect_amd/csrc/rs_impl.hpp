@@ -591,6 +591,105 @@ __device__ __forceinline__ void gf_combine(const uint4 (&x)[K], const uint32_t* 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Encodes with ISA-L's Cauchy generator (gf_gen_cauchy1_matrix,
+// EC/erasure_coder.c:43): parity row i, data column j holds inv(i ^ j), so for
+// k a multiple of 4 every 4 x 4 block of the parity rows (rows k+a, columns
+// 4g+c) is XOR-circulant: M[a][c] = h(a ^ c) with h(t) = M[0][4g+t].  Over
+// GF(2^8) (characteristic 2) such a block applies with 9 constant
+// multiplications instead of 16, a two-level Karatsuba over the index bits:
+//   s = x0^x1^x2^x3, u = x1^x3, v = x2^x3,
+//   y0 = h0 s ^ (h0^h1) u ^ (h0^h2) v ^ H x3
+//   y1 = h1 s ^ (h0^h1) u ^ (h1^h3) v ^ H x3
+//   y2 = h2 s ^ (h2^h3) u ^ (h0^h2) v ^ H x3
+//   y3 = h3 s ^ (h2^h3) u ^ (h1^h3) v ^ H x3        (H = h0^h1^h2^h3)
+// (expand each y and the x terms cancel pairwise to y_a = sum_c h(a^c) x_c).
+// Per dword of a group: 27 v_perm + 3 pre-XORs + 4 selector sets + 19 XORs =
+// 65 VALU ops against 88 for the general 16-coefficient form.  RS(12,8)
+// encode was VALU-bound at 80 % VALU busy and a 1.89 GHz clock
+// (profiles/r04/sq_bound_pmc.txt); the block's tables: cauchy_tables().
+// Bytes are identical: the same products, reassociated.
+// ---------------------------------------------------------------------------
+constexpr int kCauchyTabs = 9;  // tables per 4-column group: h0, h1, h0^h1, h2, h3, h2^h3, h0^h2, h1^h3, H
+
+template <int K>
+__device__ __forceinline__ void gf_combine_cauchy4(const uint4 (&x)[K], const uint32_t* tl, uint4 (&acc)[4])
+{
+    static_assert(K % 4 == 0, "4-column groups");
+#pragma unroll
+    for (int g = 0; g < K / 4; ++g) {
+        uint4 q[kCauchyTabs];
+        uint32_t t2[kCauchyTabs];
+#pragma unroll
+        for (int i = 0; i < kCauchyTabs; ++i) {
+            const uint32_t* t = &tl[(g * kCauchyTabs + i) * kTabStride];
+            q[i] = *reinterpret_cast<const uint4*>(t);
+            t2[i] = t[4];
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t x0 = lane_word(x[4 * g + 0], w), x1 = lane_word(x[4 * g + 1], w);
+            const uint32_t x2 = lane_word(x[4 * g + 2], w), x3 = lane_word(x[4 * g + 3], w);
+            const uint32_t u = x1 ^ x3, v = x2 ^ x3, sm = xor3(x0, x1, v);
+            const Sel ss = selectors(sm), su = selectors(u), sv = selectors(v), s3 = selectors(x3);
+            auto lk = [&](int i, const Sel& sl, int f) {  // field f of table i at the selectors
+                return f == 0 ? __builtin_amdgcn_perm(q[i].y, q[i].x, sl.s0)
+                              : f == 1 ? __builtin_amdgcn_perm(q[i].w, q[i].z, sl.s1)
+                                       : __builtin_amdgcn_perm(t2[i], t2[i], sl.s2);
+            };
+            auto mul = [&](int i, const Sel& sl) { return xor3(lk(i, sl, 0), lk(i, sl, 1), lk(i, sl, 2)); };
+            const uint32_t m_u01 = mul(2, su), m_u23 = mul(5, su);   // (h0^h1) u, (h2^h3) u
+            const uint32_t m_v02 = mul(6, sv), m_v13 = mul(7, sv);   // (h0^h2) v, (h1^h3) v
+            const uint32_t m_h = mul(8, s3);                          // H x3
+            const uint32_t e02 = m_v02 ^ m_h, e13 = m_v13 ^ m_h;
+            const uint32_t z[4] = {m_u01 ^ e02, m_u01 ^ e13, m_u23 ^ e02, m_u23 ^ e13};
+            const int hs[4] = {0, 1, 3, 4};  // tables of h0..h3
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const uint32_t y = g == 0 ? xor3(lk(hs[a], ss, 0), lk(hs[a], ss, 1), lk(hs[a], ss, 2)) ^ z[a]
+                                          : xor3(xor3(lane_word(acc[a], w), lk(hs[a], ss, 0), lk(hs[a], ss, 1)),
+                                                 lk(hs[a], ss, 2), z[a]);
+                set_word(acc[a], w, y);
+            }
+        }
+    }
+}
+
+// Host: whether rows r0..r0+3 of p's coefficients are XOR-circulant in every
+// 4-column group (M[r0+a][4g+c] == M[r0][4g+(a^c)]), and their tables in the
+// order gf_combine_cauchy4 reads them (kCauchyTabs per group, flattened).
+inline bool cauchy_blocks(const uint8_t* coef, int cols, int r0, int rows)
+{
+    if (rows != 4 || cols % 4) return false;
+    for (int g = 0; g < cols / 4; ++g)
+        for (int a = 0; a < 4; ++a)
+            for (int c = 0; c < 4; ++c)
+                if (coef[(r0 + a) * cols + 4 * g + c] != coef[r0 * cols + 4 * g + (a ^ c)]) return false;
+    return true;
+}
+
+inline void cauchy_tables(const uint8_t* coef, int cols, int r0, gf::PermTable* out)
+{
+    for (int g = 0; g < cols / 4; ++g) {
+        const uint8_t* h = &coef[r0 * cols + 4 * g];
+        const uint8_t m[kCauchyTabs] = {h[0], h[1], static_cast<uint8_t>(h[0] ^ h[1]), h[2], h[3],
+                                        static_cast<uint8_t>(h[2] ^ h[3]), static_cast<uint8_t>(h[0] ^ h[2]),
+                                        static_cast<uint8_t>(h[1] ^ h[3]),
+                                        static_cast<uint8_t>(h[0] ^ h[1] ^ h[2] ^ h[3])};
+        for (int i = 0; i < kCauchyTabs; ++i) out[g * kCauchyTabs + i] = gf::perm_table(m[i]);
+    }
+}
+
+// ELECT_EC_CAUCHY=0 turns the structured form off (A/B); on by default.
+inline bool cauchy_enabled()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("ELECT_EC_CAUCHY");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
 // Stage the byte-shuffle tables of a launch into LDS (8 dwords per coefficient).
 template <int K, int R>
 __device__ __forceinline__ void stage_tables(const gf::PermTable (&tab)[R][K], uint32_t* tl)
@@ -795,6 +894,30 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16u(const FastArgs<K, R> a)
             }
         }
     }
+}
+
+// The Cauchy-structured plain encode (gf_combine_cauchy4): gf_apply_x16u's
+// scalar-base form with the 9-multiplication combine.  92 VGPRs (the nine
+// tables of a group live in VGPRs), so 20 waves per CU; asking the allocator
+// for 6 / 7 / 8 waves per SIMD spilled 45 / 99 / 103 VGPRs, and the occupancy
+// sweep (profiles/r05/rs12_cauchy_ab.txt) is flat above 16 waves per CU.
+template <int K>
+__global__ __launch_bounds__(kBlock) void gf_apply_x16c(const FastArgs<K, 4> a)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tl[4 * K * kTabStride];
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t first = __builtin_amdgcn_readfirstlane(idx);
+    const uint32_t stripe = div_magic(first, a.magic, a.shift);
+    const uint32_t off = (idx - stripe * a.segs) * 16u;
+    stage_tables<K, 4>(a.tab, tl);
+    if (first >= a.total) return;
+    uint4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + static_cast<uint64_t>(stripe) * a.ss[j] + off);
+    uint4 acc[4];
+    gf_combine_cauchy4<K>(x, tl, acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) store_nt(a.dp[r] + static_cast<uint64_t>(stripe) * a.ds[r] + off, acc[r]);
 }
 
 // Padded launches with per-stripe content lengths, no hash, and L % 16 == 0:
@@ -1017,7 +1140,12 @@ inline LaunchShape launch_shape(Family f, int cols, int rows, uint64_t len, bool
     const bool write_heavy = 2 * rows >= cols;
     const bool wide = cols * rows >= 16;
     // the plain caps for blocks of more than one wave
-    const int multi_cap = write_heavy ? P.write_waves : (cols >= 8 && rows >= 2) ? P.read_wide_waves : P.read_waves;
+    // ELECT_EC_WRITE_WAVES overrides P.write_waves (A/B only)
+    static const int write_waves = [] {
+        const char* e = std::getenv("ELECT_EC_WRITE_WAVES");
+        return e ? std::atoi(e) : kPolicy.write_waves;
+    }();
+    const int multi_cap = write_heavy ? write_waves : (cols >= 8 && rows >= 2) ? P.read_wide_waves : P.read_waves;
     const int one_wave_cap = write_heavy ? P.one_wave_write_waves
                              : cols >= 8 ? P.one_wave_read_wide_waves
                                          : P.one_wave_read_waves;
@@ -1167,6 +1295,15 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                             hipLaunchKernelGGL((gf_apply_x16u<K, R, false, true>), grid, dim3(sh.block), lds_d, stream, a);
                         else
                             hipLaunchKernelGGL((gf_apply_x16<K, R, false, false, true>), grid, dim3(sh.block), lds_d, stream, a);
+                        launched = true;
+                    }
+                }
+                if constexpr (R == 4 && K % 4 == 0 && K >= kPolicy.scalar_base_min_cols) {
+                    // Cauchy-generator encodes: the 9-multiplication form (gf_combine_cauchy4)
+                    if (!launched && scalar_base && cauchy_enabled() && cauchy_blocks(p.coef, p.cols, r0, R)) {
+                        FastArgs<K, R> ac = a;
+                        cauchy_tables(p.coef, p.cols, r0, &ac.tab[0][0]);
+                        hipLaunchKernelGGL((gf_apply_x16c<K>), grid, dim3(sh.block), lds, stream, ac);
                         launched = true;
                     }
                 }

@@ -148,6 +148,14 @@ for step in "$@"; do
             ELECT_EC_DISPATCH_BLOCKING=$b run "bench_hostpath_blk${b}_${alloc}_T64_$i" 300 python bench.py --config hostpath \
                 --threads 64 --host-alloc $alloc --host-seconds 2 --steps 8 || exit $?
         done; done; done ;;
+    cauchycap)  # RS(12,8) encode vs the occupancy cap (ELECT_EC_WRITE_WAVES), both forms, interleaved
+        for i in 1 2; do for w in ${CAPS:-12 16 20 24}; do for c in 1 0; do
+            ELECT_EC_WRITE_WAVES=$w ELECT_EC_CAUCHY=$c run "bench_rs12_cap${w}_cauchy${c}_$i" 300 python bench.py --config rs12 --steps 50 || exit $?
+        done; done; done ;;
+    cauchyab)  # RS(12,8) encode: the XOR-circulant 9-multiplication form (ELECT_EC_CAUCHY=1) vs the general one, interleaved
+        for i in 1 2 3; do for c in 1 0; do
+            ELECT_EC_CAUCHY=$c run "bench_rs12_cauchy${c}_$i" 300 python bench.py --config rs12 --steps ${CAB_STEPS:-50} ${CAB_ARGS:-} || exit $?
+        done; done ;;
     hostprof)  # kernel trace of the pageable host path at 64 callers (gather / code / scatter durations)
         run hostprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/hostprof_$TAG -o run \
             -- python3 bench.py --config hostpath --threads 64 --host-seconds 2 --steps 8 || exit $? ;;
