@@ -1221,6 +1221,34 @@ def config_update(args, world, rank, dev):
                        "parallelism": f"stripe-partitioned x{world}"}}
 
 
+def mix_ceiling(srcs, dsts, L: int, lens=None, reps: int = 5) -> dict:
+    """The access pattern of a coding launch without its GF arithmetic
+    (elect_ec_mix_probe): inputs `srcs` (each [S, L]-strided uint8 views, the
+    kernel's columns), content lengths `lens` ([S, len(srcs)] int32 on the device,
+    or None), XORed into `dsts`.  Best of 64 / 128 / 256-thread blocks, median of
+    `reps` launches each, HIP events.  Returns {"ms", "block"}: what a kernel of
+    this shape could reach here; a kernel's frac_of_mix = this ms / its ms."""
+    from elect_amd import _lib
+    S = srcs[0].shape[0]
+    lp = lens.to(torch.int32).contiguous() if lens is not None else None
+    best = None
+    for block in (64, 128, 256):
+        ts = []
+        for _ in range(reps + 1):
+            e0, e1 = Event(), Event()
+            e0.record()
+            _lib.mix_probe([(t.data_ptr(), t.stride(0)) for t in srcs], [(t.data_ptr(), t.stride(0)) for t in dsts],
+                           L, S, lp.data_ptr() if lp is not None else 0, block,
+                           stream=torch.cuda.current_stream().cuda_stream)
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        ms = sorted(ts[1:])[reps // 2]
+        if best is None or ms < best["ms"]:
+            best = {"ms": round(ms, 4), "block": block}
+    return best
+
+
 def config_padded(args, world, rank, dev):
     """encode with implicit zero padding, RS(6,4), 64 KiB
     codeLength, content lengths uniform in [0, L] (mean 50 % fill)."""
@@ -1249,6 +1277,9 @@ def config_padded(args, world, rank, dev):
     valid = int(lens.sum().item())
     alg = valid + B * m * L  # bytes actually needed: valid data + full parity
     gbs = alg / (ms * 1e-3) / 1e9
+    # the same read:write mix (content prefixes in, full parity out) without the GF work
+    mix = mix_ceiling([data[:, j] for j in range(k)], [ref[:, r] for r in range(m)], L, lens)
+    mix["frac_of_mix"] = round(mix["ms"] / ms, 4)
     return {"metric": "GiB/s device-resident RS(6,4) zero-padded encode, 64 KiB codeLength",
             "value": round(world * args.steps * B * k * L / dt / GIB, 2), "unit": "GiB/s (codeLength bytes)",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -1257,7 +1288,8 @@ def config_padded(args, world, rank, dev):
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                          "kernel": "gf_apply_lens<4,2,2> (padded, per-stripe lengths)", "algorithmic_bytes_per_launch": alg,
-                         "fill": round(valid / (B * k * L), 3)},
+                         "fill": round(valid / (B * k * L), 3), "mix_probe": mix,
+                         "frac_of_mix": mix["frac_of_mix"]},
             "config": {"workload": f"{B} stripes, content lengths " + (f"uniform in [0, {L}]" if args.pad_fill == "random"
                                                                      else f"{args.pad_fill} x {L}"),
                        "parallelism": f"stripe-partitioned x{world}"}}
@@ -1432,12 +1464,33 @@ def config_flows(args, world, rank, dev):
         pe.append(e0.elapsed_time(e1))
     plain_ms = sorted(pe)[4]
     plain_alg = data.shape[0] * n * data.shape[2]
+    # each step's own read:write mix without its GF work and hash (elect_ec_mix_probe), on the
+    # same buffers and content lengths (tiled: each tile's share of its unit's)
+    if tile:
+        Lc = tile
+
+        def coding_lens(lg):  # [B, c] logical lengths -> [B*T, c] per tile
+            t_off = torch.arange(T, device=dev, dtype=torch.int64).view(1, T, 1) * tile
+            return (lg.to(torch.int64).view(B, 1, -1) - t_off).clamp(0, tile).view(B * T, -1).to(torch.int32)
+        old_col, dec_in = view[:, t], [view[:, j] for j in surv]
+    else:
+        Lc = L
+
+        def coding_lens(lg):
+            return lg.to(torch.int32)
+        old_col, dec_in = data[:, t], [stripe[:, j] for j in surv]
+    full = torch.full((ulens.shape[0], m), L, dtype=torch.int32, device=dev)
+    mixes = {"encode": mix_ceiling([data[:, j] for j in range(k)], [par[:, r] for r in range(m)], Lc, coding_lens(lens)),
+             "update": mix_ceiling([old_col, new] + [par[:, r] for r in range(m)], [par_new[:, r] for r in range(m)], Lc,
+                                   coding_lens(torch.cat([ulens, full], 1))),
+             "decode": mix_ceiling(dec_in, [rebuilt[:, 0]], Lc, coding_lens(dlens))}
     alg = {"encode": valid + B * m * L, "update": uvalid + 2 * B * m * L, "decode": dvalid + B * L}
     kern = {}
     for nm in ("encode", "update", "decode"):
         gbs = alg[nm] / (ms[nm] * 1e-3) / 1e9
         kern[nm] = {"ms": round(ms[nm], 4), "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-                    "algorithmic_bytes_per_launch": alg[nm]}
+                    "algorithmic_bytes_per_launch": alg[nm], "mix_probe": mixes[nm],
+                    "frac_of_mix": round(mixes[nm]["ms"] / ms[nm], 4)}
     return {"metric": "GiB/s device-resident ELECT coding steps (padded+hashed encode, padded+hashed update, "
                       "padded degraded-read decode), RS(6,4)",
             "value": round(world * args.steps * B * (2 * k + 1) * L / dt / GIB, 2),

@@ -77,6 +77,9 @@ SIGNATURES = [
     ("elect_ec_set_host_devices", ctypes.c_int, [_ip, ctypes.c_int]),
     ("elect_ec_set_batching", ctypes.c_int, [ctypes.c_int, ctypes.c_uint, ctypes.c_size_t]),
     ("elect_ec_host_path_stats", ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
+    ("elect_ec_mix_probe", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
+                                          ctypes.POINTER(ColumnT), _cp, ctypes.POINTER(ColumnT), ctypes.c_int,
+                                          ctypes.c_int, _cp]),
     ("elect_ec_host_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(_cp)]),
     ("elect_ec_host_free", ctypes.c_int, [_cp]),
     ("elect_ec_host_pinned", ctypes.c_int, [_cp, ctypes.c_size_t]),
@@ -208,6 +211,16 @@ def hbm_probe(kind: int, src: int, dst: int, nbytes: int, block: int = 256, wave
     """Enqueue one HBM ceiling probe (elect_ec_hbm_probe): kind 0 read, 1 write, 2 copy, 3 / 4 the
     decode- / encode-shaped stream mixes (4 streams in, 1 / 2 out); | 0x100 for XCD-major order."""
     check(lib.elect_ec_hbm_probe(kind, src or None, dst, nbytes, block, waves_per_cu, stream or None), "hbm_probe")
+
+
+def mix_probe(src, dst, chunk_size: int, stripes: int, lengths: int = 0, block: int = 256, waves_per_cu: int = 0,
+              stream: int = 0) -> None:
+    """Enqueue one stream-mix ceiling probe (elect_ec_mix_probe): src / dst are (ptr, stripe_stride) pairs,
+    lengths a device address of [stripes][len(src)] uint32 content lengths or 0."""
+    s = (ColumnT * len(src))(*[ColumnT(p, st) for p, st in src])
+    d = (ColumnT * len(dst))(*[ColumnT(p, st) for p, st in dst])
+    check(lib.elect_ec_mix_probe(len(src), len(dst), chunk_size, stripes, s, lengths or None, d, block, waves_per_cu,
+                                 stream or None), "mix_probe")
 
 
 def set_host_devices(devices) -> None:

@@ -282,6 +282,19 @@ int elect_ec_hbm_probe(int kind, const void* src, void* dst, size_t bytes, int b
         elect::kern::hbm_probe(kind, src, dst, bytes, block, waves_per_cu, static_cast<hipStream_t>(stream)));
 }
 
+int elect_ec_mix_probe(int num_in, int num_out, size_t chunk_size, size_t num_stripes, const elect_ec_column* src,
+                       const uint32_t* lengths, const elect_ec_column* dst, int block, int waves_per_cu, void* stream)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ELECT_EC_ENODEV;
+    if (!src || !dst || num_in < 1 || num_in > 8 || num_out < 1 || num_out > 4) return ELECT_EC_EINVAL;
+    elect::kern::Column s[8], d[4];
+    for (int j = 0; j < num_in; ++j) s[j] = elect::host::col(src[j].ptr, src[j].stripe_stride, 0);
+    for (int r = 0; r < num_out; ++r) d[r] = elect::host::col(dst[r].ptr, dst[r].stripe_stride, 0);
+    return elect::host::map_hip(elect::kern::mix_probe(num_in, num_out, chunk_size, num_stripes, s, lengths, d, block,
+                                                       waves_per_cu, static_cast<hipStream_t>(stream)));
+}
+
 int elect_ec_device_count(int* count)
 {
     if (!count) return ELECT_EC_EINVAL;

@@ -547,6 +547,79 @@ hipError_t launch_copy_pieces(const CopyPiece* pieces, uint32_t n, hipStream_t s
     return hipGetLastError();
 }
 
+// Stream-mix ceiling probe (elect_ec_mix_probe): the access pattern of a coding
+// launch with the GF arithmetic taken out.  NIN input columns, NOUT output
+// columns, one 16-byte segment per lane of whole segments; an input with a
+// content length reads only its content (the segment holding the end whole,
+// masked), as the padded kernels do; every output is the XOR of the inputs.
+// What a kernel of that shape could reach on this device: the bench reports
+// the padded and fused-step kernels as fractions of it.
+struct MixArgs {
+    const uint8_t* sp[8];
+    uint64_t ss[8];
+    uint8_t* dp[4];
+    uint64_t ds[4];
+    const uint32_t* lens;  // [stripe][nin] or null (every input whole)
+    uint32_t segs, total, magic, shift, len32;
+};
+
+template <int NIN, int NOUT>
+__global__ __launch_bounds__(kBlock) void mix_probe_kernel(const MixArgs a)
+{
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.total) return;
+    const uint32_t stripe = static_cast<uint32_t>((static_cast<uint64_t>(idx) * a.magic) >> a.shift);
+    const uint32_t off = (idx - stripe * a.segs) * 16u;
+    uint4 x = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NIN; ++j) {
+        const uint32_t valid = a.lens ? min(a.lens[static_cast<uint64_t>(stripe) * NIN + j], a.len32) : a.len32;
+        if (off >= valid) continue;
+        uint4 v = load_nt(a.sp[j] + stripe * a.ss[j] + off);
+        if (off + 16 > valid) v = keep_bytes(v, valid - off);
+        x = make_uint4(x.x ^ v.x, x.y ^ v.y, x.z ^ v.z, x.w ^ v.w);
+    }
+#pragma unroll
+    for (int r = 0; r < NOUT; ++r) store_nt(a.dp[r] + stripe * a.ds[r] + off, make_uint4(x.x + r, x.y, x.z, x.w));
+}
+
+hipError_t mix_probe(int nin, int nout, uint64_t len, uint64_t stripes, const Column* src, const uint32_t* lens,
+                     const Column* dst, int block, int waves, hipStream_t stream)
+{
+    (void)hipGetLastError();
+    if (nin < 1 || nin > 8 || nout < 1 || nout > 4 || (block != 64 && block != 128 && block != 256) || waves < 0)
+        return hipErrorInvalidValue;
+    const uint64_t segs = len / 16;
+    if (segs == 0 || stripes == 0) return hipSuccess;
+    if (segs * stripes > kMaxIndex || len > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    MixArgs a{};
+    for (int j = 0; j < nin; ++j) {
+        a.sp[j] = src[j].ptr;
+        a.ss[j] = src[j].stride;
+    }
+    for (int r = 0; r < nout; ++r) {
+        a.dp[r] = const_cast<uint8_t*>(dst[r].ptr);
+        a.ds[r] = dst[r].stride;
+    }
+    a.lens = lens;
+    a.segs = static_cast<uint32_t>(segs);
+    a.total = static_cast<uint32_t>(segs * stripes);
+    const Magic mg = make_magic(a.segs);
+    a.magic = mg.m;
+    a.shift = mg.p;
+    a.len32 = static_cast<uint32_t>(len);
+    const dim3 grid((a.total + block - 1) / block);
+    const size_t lds = cap_lds(block, 0, waves);
+    switch (nin * 10 + nout) {
+    case 41: hipLaunchKernelGGL((mix_probe_kernel<4, 1>), grid, dim3(block), lds, stream, a); break;
+    case 42: hipLaunchKernelGGL((mix_probe_kernel<4, 2>), grid, dim3(block), lds, stream, a); break;
+    case 82: hipLaunchKernelGGL((mix_probe_kernel<8, 2>), grid, dim3(block), lds, stream, a); break;
+    case 84: hipLaunchKernelGGL((mix_probe_kernel<8, 4>), grid, dim3(block), lds, stream, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 bool apply_is_aligned(const ApplyParams& p)
 {
     for (int j = 0; j < p.cols; ++j)

@@ -152,5 +152,11 @@ bool unaligned_vector_ok();
 // 256 bytes); 1: write `bytes` of dst; 2: copy src -> dst.
 hipError_t hbm_probe(int kind, const void* src, void* dst, size_t bytes, int block, int waves, hipStream_t stream);
 
+// Stream-mix ceiling probe (elect_ec_mix_probe): nin inputs (4 or 8; optional
+// content lengths [stripe][nin], device) XORed into nout outputs (1, 2 or 4),
+// whole 16-byte segments of len bytes, `block`-thread blocks, <= waves per CU.
+hipError_t mix_probe(int nin, int nout, uint64_t len, uint64_t stripes, const Column* src, const uint32_t* lens,
+                     const Column* dst, int block, int waves, hipStream_t stream);
+
 }  // namespace kern
 }  // namespace elect

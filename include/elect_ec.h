@@ -99,6 +99,18 @@ int elect_ec_unaligned_vector_ok(int* ok);
 int elect_ec_hbm_probe(int kind, const void* src, void* dst, size_t bytes, int block, int waves_per_cu,
                        void* stream);
 
+/* Stream-mix ceiling probe (diagnostics): the access pattern of a coding
+ * launch without its GF arithmetic.  num_in input columns (4 or 8), each
+ * reading only its content when `lengths` (device, [stripe][num_in] uint32) is
+ * given (the padded kernels' pattern: content only, the segment holding the
+ * end read whole and masked), XORed into num_out output columns (1, 2 or 4)
+ * written in full, over whole 16-byte segments of chunk_size bytes,
+ * `block`-thread blocks (64, 128, 256), at most waves_per_cu waves per CU
+ * (0: uncapped).  bench.py reports the padded and fused-step kernels as
+ * fractions of it.  No reference counterpart. */
+int elect_ec_mix_probe(int num_in, int num_out, size_t chunk_size, size_t num_stripes, const elect_ec_column* src,
+                       const uint32_t* lengths, const elect_ec_column* dst, int block, int waves_per_cu, void* stream);
+
 /* Devices for the host-memory calls.  By default a calling thread uses its
  * current HIP device.  With a device list, each calling thread is assigned one
  * device of the list (round robin, on its first call) and keeps it, so one

@@ -328,6 +328,8 @@ for step in "$@"; do
         run cfg_padded 400 python bench.py --config padded || exit $?
         run cfg_hashed 400 python bench.py --config hashed || exit $?
         run cfg_flows_elect 400 python bench.py --config flows --chunk 4404020 --stripes 256 || exit $?
+        run cfg_flows_elect_untiled 400 python bench.py --config flows --chunk 4404020 --stripes 256 --flows-tile 0 || exit $?
+        run cfg_flows_64k 400 python bench.py --config flows || exit $?
         run cfg_hostpath_T64 400 python bench.py --config hostpath --threads 64 --host-seconds 2 || exit $?
         run cfg_hostpath_T64_pinned 400 python bench.py --config hostpath --threads 64 --host-seconds 2 --host-alloc pinned || exit $? ;;
     padfill)  # padded encode vs content fill: where the time goes
