@@ -300,35 +300,37 @@ uint64_t thread_cpu_ns()
     return static_cast<uint64_t>(t.tv_sec) * 1000000000ull + static_cast<uint64_t>(t.tv_nsec);
 }
 
-// The HSA agent of HIP device `dev` (matched by PCI location), for
-// hsa_amd_memory_lock.  False when it cannot be found.
+// The HSA agent of HIP device `dev`, for hsa_amd_memory_lock: the one GPU
+// agent at the device's PCI domain:bus:device.function.  False when none or
+// more than one matches (partitioned GPUs could share a location): the
+// callers then take the staged path rather than lock for a wrong agent.
 bool hsa_agent_of(int dev, hsa_agent_t* out)
 {
     struct Found {
         uint32_t bdf = 0, domain = 0;
-        bool ok = false;
+        int matches = 0;
         hsa_agent_t agent{};
     };
     static std::mutex mu;
-    static std::map<int, hsa_agent_t> cache;
+    static std::map<int, std::pair<bool, hsa_agent_t>> cache;  // (found, agent), failures too
     std::lock_guard<std::mutex> lock(mu);
     auto it = cache.find(dev);
     if (it != cache.end()) {
-        *out = it->second;
-        return true;
+        *out = it->second.second;
+        return it->second.first;
     }
     static const bool init = hsa_init() == HSA_STATUS_SUCCESS;  // (reference counted: the HIP runtime holds one)
     if (!init) return false;
-    int bus = 0, device = 0, domain = 0;
-    if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, dev) != hipSuccess ||
-        hipDeviceGetAttribute(&device, hipDeviceAttributePciDeviceId, dev) != hipSuccess ||
-        hipDeviceGetAttribute(&domain, hipDeviceAttributePciDomainID, dev) != hipSuccess) {
+    char loc[64] = {};
+    unsigned domain = 0, bus = 0, device = 0, function = 0;
+    if (hipDeviceGetPCIBusId(loc, sizeof loc, dev) != hipSuccess ||
+        std::sscanf(loc, "%x:%x:%x.%x", &domain, &bus, &device, &function) != 4) {
         (void)hipGetLastError();
         return false;
     }
     Found f;
-    f.bdf = (static_cast<uint32_t>(bus) << 8) | (static_cast<uint32_t>(device) << 3);
-    f.domain = static_cast<uint32_t>(domain);
+    f.bdf = (bus << 8) | (device << 3) | function;
+    f.domain = domain;
     hsa_iterate_agents(
         [](hsa_agent_t a, void* arg) -> hsa_status_t {
             auto* f = static_cast<Found*>(arg);
@@ -338,14 +340,14 @@ bool hsa_agent_of(int dev, hsa_agent_t* out)
                 return HSA_STATUS_SUCCESS;
             hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
             hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &domain);
-            if ((bdf & ~7u) != f->bdf || domain != f->domain) return HSA_STATUS_SUCCESS;
+            if (bdf != f->bdf || domain != f->domain) return HSA_STATUS_SUCCESS;
             f->agent = a;
-            f->ok = true;
-            return HSA_STATUS_INFO_BREAK;
+            ++f->matches;
+            return HSA_STATUS_SUCCESS;
         },
         &f);
-    if (!f.ok) return false;
-    cache[dev] = f.agent;
+    cache[dev] = {f.matches == 1, f.agent};
+    if (f.matches != 1) return false;
     *out = f.agent;
     return true;
 }
@@ -386,7 +388,9 @@ public:
             if (next != live_.begin()) {
                 auto prev = std::prev(next);
                 if (prev->second.end > lo) {
-                    if (prev->first != lo || prev->second.end != hi || prev->second.kind != kind) return false;
+                    // shared only when made for the same device: a lock maps the pages for one agent
+                    if (prev->first != lo || prev->second.end != hi || prev->second.kind != kind || prev->second.dev != dev)
+                        return false;
                     same = &prev->second;
                 }
             }
@@ -399,7 +403,7 @@ public:
             if (same->state == Entry::kRetiring) return false;
             changed_.wait(lock);  // its maker is registering it: wait for the outcome
         }
-        live_.emplace(lo, Entry{hi, 0, Entry::kPending, kind, 0});
+        live_.emplace(lo, Entry{hi, 0, Entry::kPending, kind, 0, dev});
         lock.unlock();
         const uint64_t t0 = thread_cpu_ns();
         void* p = reinterpret_cast<void*>(lo);
@@ -468,6 +472,7 @@ private:
         enum State { kPending, kLive, kRetiring } state;
         Kind kind;
         uintptr_t dev_lo;
+        int dev;
     };
 
     // The HIP runtime already knows this address (registered or allocated by anyone).
@@ -1746,7 +1751,7 @@ struct ZeroCopy {
         Registrar& reg = Registrar::get();
         size_t locked = 0;
         for (; locked < rs.size(); ++locked)
-            if (!reg.acquire(rs[locked].first, rs[locked].second, Registrar::kHipRegister)) break;
+            if (!reg.acquire(rs[locked].first, rs[locked].second, Registrar::kHipRegister, dev)) break;
         int rc = kFallback;
         if (locked == rs.size()) {
             ApplyParams p;
