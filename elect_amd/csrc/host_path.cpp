@@ -1587,7 +1587,7 @@ private:
                 n += bytes;
                 return;
             }
-            flush();
+            (void)flush();
             dst = t;
             src = f;
             n = bytes;

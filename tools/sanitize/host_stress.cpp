@@ -269,6 +269,20 @@ int main(int argc, char** argv)
                     static_cast<unsigned long long>(st[4]), g_fail.load());
         CHECK(st[4] > 0, "no call took the direct path\n");
     }
+    {  // many callers on multi-MB pageable units: interior pages locked per call (round 5), ends staged,
+       // gather / scatter kernels; the registry's refcounts and exact-base releases under concurrency
+        elect_ec_set_batching(1, 0, size_t{64} << 20);
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t) th.emplace_back(worker, c, 4, 2, t + 400, iters, size_t{2400000}, false);
+        for (auto& x : th) x.join();
+        uint64_t st[8] = {};
+        elect_ec_host_path_stats(st, 8);
+        std::printf("locked pageable units: %d threads x %d iterations, locked calls %llu, unlock failures %llu, "
+                    "failures so far %d\n", threads, iters, static_cast<unsigned long long>(st[5]),
+                    static_cast<unsigned long long>(st[7]), g_fail.load());
+        CHECK(st[5] > 0, "no call took the locked path\n");
+        CHECK(st[7] == 0, "an unlock failed\n");
+    }
     {
         std::vector<std::thread> th;
         for (int t = 0; t < threads; ++t) th.emplace_back(device_worker, c, 4, 2, t, iters);
