@@ -506,6 +506,22 @@ public:
         cv_.wait(lock, [&] { return free_ > 0; });
         --free_;
     }
+    bool try_take()
+    {
+        std::lock_guard<std::mutex> lock(mu_);
+        if (free_ <= 0) return false;
+        --free_;
+        return true;
+    }
+    // ELECT_EC_REGISTER_WAIT=0: a caller finding every slot busy is staged instead of waiting (A/B)
+    static bool wait()
+    {
+        static const bool w = [] {
+            const char* e = std::getenv("ELECT_EC_REGISTER_WAIT");
+            return !(e && std::atoi(e) == 0);
+        }();
+        return w;
+    }
     void give()
     {
         {
@@ -553,6 +569,42 @@ bool direct_by_kernel()
     return k;
 }
 
+// ELECT_EC_DIRECT_MOVE=sdma: the direct units' H2D by the GPU's DMA engines
+// (hsa_amd_memory_async_copy from the locked / pool memory) instead of the
+// gather kernel, whose host reads top out near 49 GB/s; the ends and the
+// scatter stay kernels.  (A/B.)
+bool direct_h2d_sdma()
+{
+    static const bool k = [] {
+        const char* e = std::getenv("ELECT_EC_DIRECT_MOVE");
+        return e && std::string(e) == "sdma";
+    }();
+    return k;
+}
+
+// A CPU agent (the source side of host-to-device HSA copies).
+bool hsa_cpu_agent(hsa_agent_t* out)
+{
+    static const std::pair<bool, hsa_agent_t> a = [] {
+        std::pair<bool, hsa_agent_t> r{false, {}};
+        if (hsa_init() != HSA_STATUS_SUCCESS) return r;
+        hsa_iterate_agents(
+            [](hsa_agent_t ag, void* arg) -> hsa_status_t {
+                hsa_device_type_t t{};
+                if (hsa_agent_get_info(ag, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+                    auto* p = static_cast<std::pair<bool, hsa_agent_t>*>(arg);
+                    *p = {true, ag};
+                    return HSA_STATUS_INFO_BREAK;
+                }
+                return HSA_STATUS_SUCCESS;
+            },
+            &r);
+        return r;
+    }();
+    *out = a.second;
+    return a.first;
+}
+
 // Per-call page locking of batched callers' pageable units (ELECT_EC_REGISTER:
 // 0 off, 1 on, the default; units of at least kMinBytes): each unit's interior
 // pages are locked with hsa_amd_memory_lock (Registrar::kHsaLock), the batch's
@@ -587,7 +639,10 @@ struct RegisterPath {
     {
         if (mode() != 1 || len < kMinBytes || !direct_by_kernel()) return false;
         RegisterSlots& slots = RegisterSlots::get();
-        slots.take();
+        if (RegisterSlots::wait())
+            slots.take();
+        else if (!slots.try_take())
+            return false;
         Registrar& reg = Registrar::get();
         bool ok = true;
         PinnedPool& pool = PinnedPool::get();
@@ -1252,6 +1307,7 @@ private:
         std::condition_variable done;  // this batch's callers wait here for kDone
         hipStream_t stream = nullptr;
         hipEvent_t h2d_done = nullptr;
+        hsa_signal_t sig{};  // counts a direct batch's outstanding HSA copies (ELECT_EC_DIRECT_MOVE=sdma)
 
         Shape shape() const
         {
@@ -1334,6 +1390,8 @@ private:
             s.pin_in_dev = static_cast<uint8_t*>(dv);
             if (e == hipSuccess) e = hipHostGetDevicePointer(&dv, s.pin_out, 0);
             s.pin_out_dev = static_cast<uint8_t*>(dv);
+            if (e == hipSuccess && direct_h2d_sdma() && hsa_signal_create(0, 0, nullptr, &s.sig) != HSA_STATUS_SUCCESS)
+                s.sig.handle = 0;
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_hash), meta);
             s.scratch_words = kern::hash_scratch_need(arena / 16);  // a batch has at most arena/16 segments
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_scratch), s.scratch_words * sizeof(uint32_t));
@@ -1460,6 +1518,19 @@ private:
         if (sh.direct && by_kernel) {
             size_t np = 0;
             bool overflow = false;
+            // sdma: the units' [lo, hi) by hsa_amd_memory_async_copy, all counted down on s.sig
+            hsa_agent_t gpu{}, cpu{};
+            const bool sdma = direct_h2d_sdma() && s.sig.handle && hsa_agent_of(s.owner->dev_, &gpu) && hsa_cpu_agent(&cpu);
+            int64_t ncopies = 0;
+            if (sdma) {
+                for (int q = 0; q < n; ++q)
+                    for (int j = 0; j < sh.cols; ++j) {
+                        const size_t i = static_cast<size_t>(q) * kern::kMaxCols + j;
+                        ncopies += d.src_hi[i] > d.src_lo[i];
+                    }
+                hsa_signal_store_screlease(s.sig, ncopies);
+            }
+            bool copy_failed = false;
             auto piece = [&](const uint8_t* from, uint8_t* to, size_t bytes) {
                 for (size_t o = 0; o < bytes; o += kern::kMaxPieceBytes) {
                     if (np == s.max_pieces) {
@@ -1477,7 +1548,13 @@ private:
                     uint8_t* const dev = s.d_in + q * in_stride + j * sh.pitch;
                     const uint8_t* const pin = s.pin_in_dev + q * in_stride + j * sh.pitch;
                     piece(pin, dev, lo);
-                    piece(d.src[i] + lo, dev + lo, hi - lo);
+                    if (!sdma)
+                        piece(d.src[i] + lo, dev + lo, hi - lo);
+                    else if (hi > lo && hsa_amd_memory_async_copy(dev + lo, gpu, d.src[i] + lo, cpu, hi - lo, 0, nullptr,
+                                                                 s.sig) != HSA_STATUS_SUCCESS) {
+                        copy_failed = true;
+                        hsa_signal_subtract_screlease(s.sig, 1);  // the copy that was never queued
+                    }
                     piece(pin + hi, dev + hi, nb - hi);
                 }
             gather_n = np;
@@ -1494,6 +1571,11 @@ private:
             scatter_n = np - gather_n;
             e = overflow ? hipErrorInvalidValue
                          : kern::launch_copy_pieces(s.pieces_dev, static_cast<uint32_t>(gather_n), s.stream);
+            if (sdma && ncopies) {  // the coding launch below reads them: wait here, off every caller's thread
+                const hsa_signal_value_t v = hsa_signal_wait_scacquire(s.sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                                                       HSA_WAIT_STATE_BLOCKED);
+                if ((v < 0 || copy_failed) && e == hipSuccess) e = hipErrorLaunchFailure;
+            }
         } else if (sh.direct) {
             Dma dma(hipMemcpyHostToDevice, s.stream);
             for (int q = 0; q < n; ++q)

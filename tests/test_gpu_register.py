@@ -130,3 +130,54 @@ def test_registered_units_back_to_back_then_device_work():
     # (a call meeting a shared lock that is being released at that moment is staged)
     assert st["registered"] >= 8 * 3 * 5 // 2 and st["per_thread"] == 0, st
     assert st["registered"] + st["batched"] == 8 * 3 * 5, st
+
+
+OVERLAP = r"""
+import json, sys, threading
+import numpy as np
+import torch
+sys.path.insert(0, ROOT)
+from elect_amd import _lib
+from elect_amd.coder import RSCoder
+from oracle import ec_oracle as orc
+
+torch.cuda.init()
+k, m, L, P = 4, 2, (1 << 20) + 333, 4096
+rng = np.random.default_rng(21)
+block = rng.integers(0, 256, 2 * k * (L + 3 * P), dtype=np.uint8)
+# caller A's data units and caller B's overlap them shifted by one page and a byte: every B interior
+# shares pages with an A interior of another extent, so whichever locks second is refused (staged)
+a_in = [block[1 + j * (L + 3 * P):][:L] for j in range(k)]
+b_in = [block[1 + P + 1 + j * (L + 3 * P):][:L] for j in range(k)]
+enc = orc.Encoder(k, m)
+want = {"a": enc.encode([x.copy() for x in a_in]), "b": enc.encode([x.copy() for x in b_in])}
+bad = []
+
+def caller(name, ins):
+    c = RSCoder(k, m)
+    for it in range(12):
+        out = [np.zeros(L, np.uint8) for _ in range(m)]
+        c.encode_host([x.ctypes.data for x in ins], [x.ctypes.data for x in out], L)
+        if not all(np.array_equal(o, w) for o, w in zip(out, want[name])):
+            bad.append(f"{name} {it}")
+
+th = [threading.Thread(target=caller, args=("a", a_in)), threading.Thread(target=caller, args=("b", b_in))]
+for x in th:
+    x.start()
+for x in th:
+    x.join()
+print("BAD " + "; ".join(bad[:4]) if bad else "OK", json.dumps(_lib.host_path_stats()))
+"""
+
+
+def test_partially_overlapping_units_of_concurrent_callers():
+    """Two callers whose input units overlap each other's pages at another extent
+    (read-only, so both results are defined): the registry never lets the two
+    locks coexist; the caller that meets the other's lock is staged, both right."""
+    code = OVERLAP.replace("ROOT", repr(ROOT))
+    env = dict(os.environ, ELECT_EC_REGISTER="1", ELECT_EC_ZEROCOPY="0")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0 and r.stdout.strip().startswith("OK"), r.stdout[-3000:] + r.stderr[-3000:]
+    st = json.loads(r.stdout.strip().split(" ", 1)[1])
+    assert st["unregister_failures"] == 0 and st["per_thread"] == 0, st
+    assert st["registered"] + st["batched"] == 24 and st["registered"] >= 1, st

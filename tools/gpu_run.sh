@@ -157,9 +157,11 @@ for step in "$@"; do
             ELECT_EC_CAUCHY=$c run "bench_rs12_cauchy${c}_$i" 300 python bench.py --config rs12 --steps ${CAB_STEPS:-50} ${CAB_ARGS:-} || exit $?
         done; done ;;
     cbench)  # the host path from C++ callers (tools/hostpath_cbench.cpp): the library's own CPU cost, no Python
-        for i in 1 2; do for rg in ${REG_MODES:-1 0}; do for T in ${T_LIST:-64 16 4}; do
-            ELECT_EC_REGISTER=$rg run "cbench_reg${rg}_T${T}_$i" 120 tools/hostpath_cbench $T 3 || exit $?
-        done; done; done ;;
+        for i in 1 2; do for rg in ${REG_MODES:-1 0}; do for T in ${T_LIST:-64 16 4}; do for v in ${CB_VARIANTS:-8:1:4}; do
+            IFS=: read sl wt re <<< "$v"  # slots : wait : realloc_every
+            ELECT_EC_REGISTER=$rg ELECT_EC_REGISTER_SLOTS=$sl ELECT_EC_REGISTER_WAIT=$wt \
+                run "cbench_reg${rg}_s${sl}_w${wt}_r${re}_T${T}_$i" 120 tools/hostpath_cbench $T 3 4404020 $re || exit $?
+        done; done; done; done ;;
     hostprof)  # kernel trace of the pageable host path at 64 callers (gather / code / scatter durations)
         run hostprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/hostprof_$TAG -o run \
             -- python3 bench.py --config hostpath --threads 64 --host-seconds 2 --steps 8 || exit $? ;;
