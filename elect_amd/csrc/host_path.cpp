@@ -1308,6 +1308,7 @@ private:
         hipStream_t stream = nullptr;
         hipEvent_t h2d_done = nullptr;
         hsa_signal_t sig{};  // counts a direct batch's outstanding HSA copies (ELECT_EC_DIRECT_MOVE=sdma)
+        bool h2d_landed = false;  // on_h2d ran for the batch in flight (under the owner's mu_)
 
         Shape shape() const
         {
@@ -1462,16 +1463,21 @@ private:
                 return s != nullptr;
             });
             if (prev && prev->state == Slab::kInFlight) {  // wait for its H2D only
-                hipEvent_t ev = prev->h2d_done;
-                lock.unlock();
-                (void)hipEventSynchronize(ev);
-                lock.lock();
+                if (h2d_by_callback()) {  // asleep until prev's on_h2d (or its end)
+                    cv_worker_.wait(lock, [&] { return prev->h2d_landed || prev->state != Slab::kInFlight; });
+                } else {
+                    hipEvent_t ev = prev->h2d_done;
+                    lock.unlock();
+                    (void)hipEventSynchronize(ev);
+                    lock.lock();
+                }
             } else {
                 const unsigned w = batch_config().window_us.load();
                 if (w) cv_worker_.wait_until(lock, s->opened + std::chrono::microseconds(w), [&] { return s->full; });
             }
             s->full = true;
             s->state = Slab::kInFlight;  // no more reservations
+            s->h2d_landed = false;
             cv_worker_.wait(lock, [&] { return s->filled == s->reserved; });
             const Shape shape = s->shape();  // under mu_: open() rewrites these for the slab's next batch
             const int n = s->reserved;
@@ -1596,6 +1602,7 @@ private:
             e = hipMemcpyAsync(s.d_lens, s.pin_lens, static_cast<size_t>(n) * sh.cols * sizeof(uint32_t),
                                hipMemcpyHostToDevice, s.stream);
         if (e == hipSuccess) e = hipEventRecord(s.h2d_done, s.stream);
+        if (e == hipSuccess && h2d_by_callback()) e = hipLaunchHostFunc(s.stream, &Batcher::on_h2d, &s);
         if (e == hipSuccess) {
             // coding stripes: the slots' tiles in order (untiled: the slots)
             ApplyParams p;
@@ -1681,6 +1688,30 @@ private:
             return e;
         }
     };
+
+    // The dispatcher's wait for a batch's inputs to land (self-clocking): a host
+    // callback behind the H2D wakes it (the default), or it polls the event
+    // (ELECT_EC_DISPATCH_WAIT=event): hipEventSynchronize spins a core for the
+    // whole H2D, ~20 ms a batch at 64 callers (round 5, 64 callers, 2 runs each:
+    // pageable units 52.8-54.3 -> 34.1-37.1 core-ms per GiB, pool units
+    // 45.6-46.0 -> 26.7-28.3, staged 195-223 -> 211-222, the same GiB/s;
+    // profiles/r05/hostpath_register_ab.txt E).
+    static bool h2d_by_callback()
+    {
+        static const bool c = [] {
+            const char* e = std::getenv("ELECT_EC_DISPATCH_WAIT");
+            return !(e && std::string(e) == "event");
+        }();
+        return c;
+    }
+
+    static void on_h2d(void* arg)  // HIP host-function callback: no HIP calls in here
+    {
+        Slab* s = static_cast<Slab*>(arg);
+        std::lock_guard<std::mutex> lock(s->owner->mu_);
+        s->h2d_landed = true;
+        s->owner->cv_worker_.notify_one();
+    }
 
     static void on_done(void* arg)  // HIP host-function callback: no HIP calls in here
     {
