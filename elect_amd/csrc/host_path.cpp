@@ -276,17 +276,19 @@ bool direct_op(const HostOp& op, size_t len)
 // registrations is refused (hipErrorInvalidValue), and hipHostUnregister
 // given an interior pointer aborts the process.
 //
-// So: (1) no two live registrations share a page — a request that meets a
-// live registration of another extent is refused here, before the runtime
-// sees it; an identical request shares the live registration (refcounted);
-// (2) every registration is released by the exact base it was made with,
-// after the last DMA or kernel using it has completed (callers release after
-// their batch's completion); (3) memory another party has registered (either
-// end of the range already known to the runtime) is never registered again;
-// (4) a failed unregister is counted (host_path_stats), never ignored
-// silently.  The batched path registers only the pages lying wholly inside a
-// unit (interior pages): those belong to that unit alone, so neighbours never
-// meet, and the <= 2 partial pages at its ends travel through the arena.
+// So, with locks (hsa_amd_memory_lock; hipHostRegister is no longer used, see
+// Registrar): (1) no two live locks share a page — a request that meets a live
+// lock of another extent (or device) is refused here, before the runtime sees
+// it; an identical request shares the live lock (refcounted); (2) every lock is
+// released by the exact base it was made with, after the last transfer or
+// kernel using it has completed (callers release after their batch's
+// completion); (3) memory another party has registered (either end of the
+// range, and for zero-copy calls either end of every unit, already known to the
+// runtime) is never locked; (4) a failed unlock is counted (host_path_stats),
+// never ignored silently.  The batched path locks only the pages lying wholly
+// inside a unit (interior pages): those belong to that unit alone, so
+// neighbours never meet, and the <= 2 partial pages at its ends travel through
+// the arena.
 // ---------------------------------------------------------------------------
 std::atomic<uint64_t> g_unregister_failures{0};
 // CPU time (ns, calling threads) spent registering, unregistering, and in the
@@ -354,85 +356,65 @@ bool hsa_agent_of(int dev, hsa_agent_t* out)
 
 class Registrar {
 public:
-    // kHipRegister: hipHostRegister(Mapped) — the zero-copy path; the HIP
-    // runtime's own transfers know the pages.  Its hipHostUnregister waits for
-    // every queued operation on the device, other streams included (7.1 ms
-    // behind another stream's 7.1 ms of copies, profiles/r05/register_overlap.txt
-    // part 3), which is why per-call hipHostRegister cannot serve concurrent
-    // callers: at 64 callers the unregister waits cost 485 core-ms per GiB.
-    // kHsaLock: hsa_amd_memory_lock for the calling device's agent — the
-    // batched path's kernels read and write the pages through the returned
-    // address; hsa_amd_memory_unlock does not wait for the device (part 4).
-    enum Kind { kHipRegister, kHsaLock };
-
+    // Locks are hsa_amd_memory_lock for the calling device's agent: the batches'
+    // kernels (and zero-copy calls) read and write the pages through the returned
+    // address, and hsa_amd_memory_unlock does not wait for the device
+    // (profiles/r05/register_overlap.txt part 4).  hipHostRegister is not used:
+    // its hipHostUnregister waits for every queued operation on the device, other
+    // streams included (part 3: 7.1 ms behind another stream's 7.1 ms of copies;
+    // 485 core-ms per GiB at 64 callers, hostpath_register_ab.txt A), and one
+    // locking mechanism keeps the two runtime layers from mapping one page twice.
     static Registrar& get()
     {
-        static Registrar* r = new Registrar();  // never destroyed: registrations may be in use at exit
+        static Registrar* r = new Registrar();  // never destroyed: locks may be in use at exit
         return *r;
     }
 
-    // A reference on a registration of exactly [lo, hi) (page aligned, lo < hi)
-    // of this kind: the identical live one, or a new one.  False (nothing held)
-    // when [lo, hi) shares a page with a registration of another extent or
-    // kind, or with memory the HIP runtime already knows, or when the runtime
-    // refuses.  *dev_lo: the device address of lo (kHsaLock).  A kHipRegister
-    // registration is made with hipHostRegisterMapped and its device pointer
-    // is looked up at once.
-    bool acquire(uintptr_t lo, uintptr_t hi, Kind kind, int dev = 0, uintptr_t* dev_lo = nullptr)
+    // A reference on a lock of exactly [lo, hi) (page aligned, lo < hi) for
+    // device dev: the identical live one, or a new one.  False (nothing held)
+    // when [lo, hi) shares a page with a lock of another extent or device, or
+    // with memory the HIP runtime already knows at either end, or when the
+    // runtime refuses.  *dev_lo: the device address of lo.
+    bool acquire(uintptr_t lo, uintptr_t hi, int dev, uintptr_t* dev_lo)
     {
         std::unique_lock<std::mutex> lock(mu_);
         for (;;) {
             Entry* same = nullptr;
-            auto next = live_.upper_bound(lo);  // first registration starting after lo
+            auto next = live_.upper_bound(lo);  // first lock starting after lo
             if (next != live_.end() && next->first < hi) return false;
             if (next != live_.begin()) {
                 auto prev = std::prev(next);
                 if (prev->second.end > lo) {
                     // shared only when made for the same device: a lock maps the pages for one agent
-                    if (prev->first != lo || prev->second.end != hi || prev->second.kind != kind || prev->second.dev != dev)
-                        return false;
+                    if (prev->first != lo || prev->second.end != hi || prev->second.dev != dev) return false;
                     same = &prev->second;
                 }
             }
             if (!same) break;
             if (same->state == Entry::kLive) {
                 ++same->refs;
-                if (dev_lo) *dev_lo = same->dev_lo;
+                *dev_lo = same->dev_lo;
                 return true;
             }
             if (same->state == Entry::kRetiring) return false;
-            changed_.wait(lock);  // its maker is registering it: wait for the outcome
+            changed_.wait(lock);  // its maker is locking it: wait for the outcome
         }
-        live_.emplace(lo, Entry{hi, 0, Entry::kPending, kind, 0, dev});
+        live_.emplace(lo, Entry{hi, 0, Entry::kPending, 0, dev});
         lock.unlock();
         const uint64_t t0 = thread_cpu_ns();
         void* p = reinterpret_cast<void*>(lo);
-        uintptr_t d_lo = 0;
-        bool ok = false;
-        if (kind == kHsaLock) {
-            hsa_agent_t agent{};
-            void* ap = nullptr;
-            ok = hsa_agent_of(dev, &agent) && !known(lo) && !known(hi - 1) &&
-                 hsa_amd_memory_lock(p, hi - lo, &agent, 1, &ap) == HSA_STATUS_SUCCESS;
-            d_lo = reinterpret_cast<uintptr_t>(ap);
-        } else {
-            ok = !known(lo) && !known(hi - 1) && hipHostRegister(p, hi - lo, hipHostRegisterMapped) == hipSuccess;
-            void* d = nullptr;  // creates the device mapping now
-            if (ok && hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
-                if (hipHostUnregister(p) != hipSuccess) g_unregister_failures.fetch_add(1);
-                ok = false;
-            }
-            d_lo = reinterpret_cast<uintptr_t>(d);
-            (void)hipGetLastError();  // a refused registration is not the thread's next call's error
-        }
+        hsa_agent_t agent{};
+        void* ap = nullptr;
+        const bool ok = hsa_agent_of(dev, &agent) && !known(lo) && !known(hi - 1) &&
+                        hsa_amd_memory_lock(p, hi - lo, &agent, 1, &ap) == HSA_STATUS_SUCCESS;
         g_register_cpu_ns.fetch_add(thread_cpu_ns() - t0);
         lock.lock();
         auto it = live_.find(lo);
         if (ok) {
             it->second.state = Entry::kLive;
             it->second.refs = 1;
-            it->second.dev_lo = d_lo;
-            if (dev_lo) *dev_lo = d_lo;
+            it->second.dev_lo = reinterpret_cast<uintptr_t>(ap);
+            *dev_lo = it->second.dev_lo;
         } else {
             live_.erase(it);
         }
@@ -440,9 +422,9 @@ public:
         return ok;
     }
 
-    // Drops a reference taken by acquire(lo, ...); the last one unregisters
-    // (by lo, the base it was registered with).  Only after every transfer and
-    // kernel touching the pages has completed.
+    // Drops a reference taken by acquire(lo, ...); the last one unlocks (by lo,
+    // the base it was locked with).  Only after every transfer and kernel
+    // touching the pages has completed.
     void release(uintptr_t lo)
     {
         std::unique_lock<std::mutex> lock(mu_);
@@ -450,15 +432,9 @@ public:
         if (it == live_.end() || it->second.state != Entry::kLive) return;
         if (--it->second.refs > 0) return;
         it->second.state = Entry::kRetiring;  // stays in the map (refusing overlaps) until it is gone
-        const Kind kind = it->second.kind;
         lock.unlock();
         const uint64_t t0 = thread_cpu_ns();
-        const bool ok = kind == kHsaLock ? hsa_amd_memory_unlock(reinterpret_cast<void*>(lo)) == HSA_STATUS_SUCCESS
-                                         : hipHostUnregister(reinterpret_cast<void*>(lo)) == hipSuccess;
-        if (!ok) {
-            g_unregister_failures.fetch_add(1);
-            (void)hipGetLastError();
-        }
+        if (hsa_amd_memory_unlock(reinterpret_cast<void*>(lo)) != HSA_STATUS_SUCCESS) g_unregister_failures.fetch_add(1);
         g_unregister_cpu_ns.fetch_add(thread_cpu_ns() - t0);
         lock.lock();
         live_.erase(lo);
@@ -470,7 +446,6 @@ private:
         uintptr_t end;
         int refs;
         enum State { kPending, kLive, kRetiring } state;
-        Kind kind;
         uintptr_t dev_lo;
         int dev;
     };
@@ -607,7 +582,7 @@ bool hsa_cpu_agent(hsa_agent_t* out)
 
 // Per-call page locking of batched callers' pageable units (ELECT_EC_REGISTER:
 // 0 off, 1 on, the default; units of at least kMinBytes): each unit's interior
-// pages are locked with hsa_amd_memory_lock (Registrar::kHsaLock), the batch's
+// pages are locked with hsa_amd_memory_lock (Registrar), the batch's
 // kernels move them over PCIe, and they are unlocked when the call's batch is
 // done.  No staging copies of the interior, no DMA engine, no device wait.
 struct RegisterPath {
@@ -657,7 +632,7 @@ struct RegisterPath {
             uintptr_t lo = 0, hi = 0;
             interior(p, n, lo, hi);
             if (hi - lo < kMinInterior) return;
-            if (!reg.acquire(lo, hi, Registrar::kHsaLock, dev, &dev_addr)) {
+            if (!reg.acquire(lo, hi, dev, &dev_addr)) {
                 ok = false;
                 return;
             }
@@ -1766,10 +1741,15 @@ Batcher* batcher(int dev)
 }
 
 // ---------------------------------------------------------------------------
-// Zero-copy calls.  A caller that is alone on its device (no other call in
-// flight, no other thread calling for 20 ms: lone_caller) has its own buffers page-locked for the duration of the call
-// (hipHostRegister), and the kernel reads its units and writes its outputs over
-// PCIe directly: no staging copies, no DMA stages, no helper threads.
+// Zero-copy calls (OFF by default since round 5: the batched path's per-call
+// locking and gather / scatter kernels serve a lone caller faster, 24.9 against
+// 19.8-20.7 GiB/s at ELECT's codeLength, and equally at two callers, 35.0 against
+// 34.5, profiles/r05/hostpath_register_ab.txt G).  A caller that is alone on its
+// device (no other call in flight, no other thread calling for 20 ms:
+// lone_caller) has its own buffers page-locked for the duration of the call
+// (hsa_amd_memory_lock since round 5, hipHostRegister before), and the kernel
+// reads its units and writes its outputs over PCIe directly: no staging copies,
+// no DMA stages, no helper threads.
 // tools/tune/zerocopy_probe.py (RS(6,4), 4,404,020 B, one caller): 35.4 GiB/s
 // against 22.1 for the staged path (register 0.02 ms and unregister 0.01 ms per
 // call; kernel 0.43 ms); through the product (bench.py --config hostpath, 2 s
@@ -1777,7 +1757,7 @@ Batcher* batcher(int dev)
 // GiB/s staged, but 2 callers 35.9 against 38.8-39.3 batched.  Concurrent
 // callers lose with it (registration contends in the driver: 7.8 + 12.6 ms per
 // call at 64 callers, and 64 kernels reading host memory at once run at 26
-// GiB/s against the batch's 44), so only a lone caller takes it.  ELECT_EC_ZEROCOPY: 0 off, 1 (default) lone callers with
+// GiB/s against the batch's 44), so only a lone caller takes it.  ELECT_EC_ZEROCOPY: 0 off (default), 1 lone callers with
 // units of at least kMinBytes, 2 every eligible call (tests).  Hashed calls keep
 // the staged path.  Any registration failure (memory already locked by another
 // call, a mapping the driver refuses) falls back to the staged path.  Units in
@@ -1793,7 +1773,7 @@ struct ZeroCopy {
     {
         static const int m = [] {
             const char* e = std::getenv("ELECT_EC_ZEROCOPY");
-            return e ? std::atoi(e) : 1;
+            return e ? std::atoi(e) : 0;
         }();
         return m;
     }
@@ -1829,6 +1809,27 @@ struct ZeroCopy {
         return m;
     }
 
+    // No unit's first or last byte is known to the HIP runtime (registered or
+    // allocated by another party): the page-rounded ranges start before and end
+    // after the units, so the registry's checks at the range ends would miss a
+    // registration of exactly a unit.
+    static bool units_unknown(const HostOp& op, size_t len)
+    {
+        auto unknown = [](const void* x) {
+            hipPointerAttribute_t a{};
+            const hipError_t e = hipPointerGetAttributes(&a, x);
+            (void)hipGetLastError();
+            return e == hipSuccess && a.type == hipMemoryTypeUnregistered;
+        };
+        for (int j = 0; j < op.cols; ++j) {
+            const size_t n = input_span(op, j, len);
+            if (op.in[j] && n && !(unknown(op.in[j]) && unknown(op.in[j] + n - 1))) return false;
+        }
+        for (int r = 0; r < op.rows; ++r)
+            if (!(unknown(op.out[r]) && unknown(op.out[r] + len - 1))) return false;
+        return true;
+    }
+
     // This thread's stream per device, destroyed when the thread exits (ELECT's
     // coding pools retire threads).
     struct ThreadStreams {
@@ -1860,11 +1861,20 @@ struct ZeroCopy {
         hipStream_t stream = ts.stream[dev];
         // through the registry: a range sharing a page with any live registration
         // (another thread's call) is refused, and the call falls back to the staged path
+        // Locked with hsa_amd_memory_lock, like the batched path's units: one locking
+        // mechanism in the process.  (Round 5: zero-copy calls registered with
+        // hipHostRegister right after batched calls had locked and unlocked pages
+        // of the same units with hsa_amd_memory_lock faulted once in the GPU suite,
+        // tests/test_gpu_parity.py::test_lone_caller_copy_fanout; the HSA runtime
+        // keeps unlocked ranges cached, and the two layers' mappings of one page
+        // are the overlap hazard of DESIGN.md §5.2 again.)
         const auto rs = pinned ? std::vector<std::pair<uintptr_t, uintptr_t>>{} : ranges(op, len);
+        if (!pinned && !units_unknown(op, len)) return kFallback;  // someone else registered a unit: staged
+        std::vector<uintptr_t> dev_lo(rs.size(), 0);
         Registrar& reg = Registrar::get();
         size_t locked = 0;
         for (; locked < rs.size(); ++locked)
-            if (!reg.acquire(rs[locked].first, rs[locked].second, Registrar::kHipRegister, dev)) break;
+            if (!reg.acquire(rs[locked].first, rs[locked].second, dev, &dev_lo[locked])) break;
         int rc = kFallback;
         if (locked == rs.size()) {
             ApplyParams p;
@@ -1873,16 +1883,24 @@ struct ZeroCopy {
             p.cols = op.cols;
             p.rows = op.rows;
             std::memcpy(p.coef, op.coef, sizeof(p.coef));
+            PinnedPool& pool = PinnedPool::get();
+            auto device_of = [&](const void* x) -> const void* {  // x inside one locked range (or the pool)
+                const uintptr_t a = reinterpret_cast<uintptr_t>(x);
+                if (pinned) return reinterpret_cast<const void*>(pool.device_addr(x));
+                for (size_t i = 0; i < rs.size(); ++i)
+                    if (a >= rs[i].first && a < rs[i].second)
+                        return reinterpret_cast<const void*>(dev_lo[i] + (a - rs[i].first));
+                return nullptr;
+            };
             bool ok = true;
             for (int j = 0; j < op.cols && ok; ++j) {
-                void* d = nullptr;
-                if (op.in[j] && (!op.lens || op.lens[j]))
-                    ok = hipHostGetDevicePointer(&d, const_cast<unsigned char*>(op.in[j]), 0) == hipSuccess;
+                const void* d = nullptr;
+                if (op.in[j] && (!op.lens || op.lens[j])) ok = (d = device_of(op.in[j])) != nullptr;
                 p.src[j] = col(d, 0, 0);
             }
             for (int q = 0; q < op.rows && ok; ++q) {
-                void* d = nullptr;
-                ok = hipHostGetDevicePointer(&d, op.out[q], 0) == hipSuccess;
+                const void* d = device_of(op.out[q]);
+                ok = d != nullptr;
                 p.dst[q] = col(d, 0, 0);
             }
             if (op.lens) {  // one stripe: the per-column content lengths ride in the kernel arguments

@@ -136,7 +136,8 @@ int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes);
 
 /* Counters of the host-memory path since the process started, for diagnostics:
  * out[0] zero-copy calls (a lone caller's buffers page-locked and coded in
- * place over PCIe; ELECT_EC_ZEROCOPY=0 off, 1 default, 2 every eligible call),
+ * place over PCIe; ELECT_EC_ZEROCOPY=0 off (the default since round 5), 1 lone
+ * callers, 2 every eligible call),
  * out[1] zero-copy attempts that fell back (registration refused), out[2]
  * calls coded through the cross-thread batcher with staging copies, out[3]
  * calls coded by the per-thread staging engine, out[4] calls coded through the

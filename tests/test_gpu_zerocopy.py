@@ -1,11 +1,12 @@
-"""Zero-copy host-memory calls (host_path.cpp ZeroCopy): a lone caller's own
-buffers are page-locked for the call and the kernel reads and writes them over
-PCIe.  Every host entry point that takes the path (encode, decode, update, the
-padded encode / update / degraded-read steps, with NULL empty units and an
-in-place update) against the CPU oracle, forced on (ELECT_EC_ZEROCOPY=2, so
-short units take it too) and by default (lone callers with units of 1 MiB and
-up); a buffer another party has already page-locked makes the library's
-registration fail, and the call must still be right (staged path).  Each mode
+"""Zero-copy host-memory calls (host_path.cpp ZeroCopy, off by default since
+round 5): a lone caller's own buffers are page-locked for the call
+(hsa_amd_memory_lock) and the kernel reads and writes them over PCIe.  Every
+host entry point that takes the path (encode, decode, update, the padded
+encode / update / degraded-read steps, with NULL empty units and an in-place
+update) against the CPU oracle, forced on (ELECT_EC_ZEROCOPY=2, so short units
+take it too) and as the lone-caller policy (ELECT_EC_ZEROCOPY=1: units of 1 MiB
+and up); a unit another party has registered keeps the library from locking
+it, and the call must still be right (staged path).  Each mode
 runs in its own process: the library reads ELECT_EC_ZEROCOPY once."""
 import os
 import subprocess
@@ -94,7 +95,8 @@ print("BAD" if bad else "OK", json.dumps(_lib.host_path_stats()))
 def _run(env_extra, lengths, prelock=False, seed=7):
     code = (SCRIPT.replace("ROOT", repr(ROOT)).replace("SEED", str(seed)).replace("LENGTHS", repr(lengths))
             .replace("PRELOCK", "True" if prelock else "False"))
-    env = dict(os.environ, **env_extra)
+    env = {k: v for k, v in os.environ.items() if k != "ELECT_EC_ZEROCOPY"}
+    env.update(env_extra)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0 and r.stdout.strip().startswith("OK"), r.stdout[-2000:] + r.stderr[-2000:]
     import json
@@ -107,11 +109,18 @@ def test_zero_copy_forced_every_entry_point():
     assert st["zero_copy"] == 5 * 6 and st["zero_copy_fallback"] == 0, st  # every call took the path
 
 
-def test_zero_copy_default_lone_caller():
-    # the default policy: a lone caller's units of 1 MiB and up (ELECT's codeLength) go zero-copy
-    st = _run({}, [1 << 20, 4404020], seed=8)
-    # decode_ex codes a prefix of L - 33 bytes: below 1 MiB at L = 1 MiB, so it is staged
+def test_zero_copy_lone_caller_policy():
+    # ELECT_EC_ZEROCOPY=1: a lone caller's units of 1 MiB and up (ELECT's codeLength) go zero-copy
+    st = _run({"ELECT_EC_ZEROCOPY": "1"}, [1 << 20, 4404020], seed=8)
+    # decode_ex codes a prefix of L - 33 bytes: below 1 MiB at L = 1 MiB, so it is batched
     assert st["zero_copy"] == 11 and st["zero_copy_fallback"] == 0, st
+
+
+def test_zero_copy_off_by_default():
+    # round 5: the batched path (units locked per call, gather / scatter kernels) serves a lone caller
+    # faster than zero-copy, so the default is off
+    st = _run({}, [4404020], seed=12)
+    assert st["zero_copy"] == 0 and st["registered"] + st["batched"] == 6, st
 
 
 def test_zero_copy_falls_back_when_memory_is_already_locked():
