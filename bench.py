@@ -176,9 +176,12 @@ def parse():
     ap.add_argument("--host-register", type=int, choices=(0, 1), default=None,
                     help="hostpath: ELECT_EC_REGISTER for the run (1: batched callers' pageable units page-locked "
                          "per call, their interior pages moved by DMA; default: the library's default)")
-    ap.add_argument("--host-op", choices=("encode", "encode_ex"), default="encode",
-                    help="hostpath: plain encode (the JNI encodeImpl), or ELECT's fused encode step "
-                         "(encodeExImpl: content = codeLength/1.05, parity hashCodes)")
+    ap.add_argument("--host-op", choices=("encode", "encode_ex", "decode", "update"), default="encode",
+                    help="hostpath: plain encode (the JNI encodeImpl), ELECT's fused encode step "
+                         "(encodeExImpl: content = codeLength/1.05, parity hashCodes), the degraded-read "
+                         "decode (decodeImpl: rebuild unit 0 from [p0, d1, d2, d3], ECRecovery.java:141) or "
+                         "the parity update (encodeUpdateImpl: [old d1, new d1, p0, p1] -> p0', p1' in place, "
+                         "ECParityUpdateVerbHandler.java:688)")
     ap.add_argument("--flows-tile", type=int, default=-1,
                     help="flows: tile bytes for the [B][T][k+m][tile] layout (-1: 64 KiB tiles above 64 KiB, "
                          "0: untiled)")
@@ -958,12 +961,19 @@ def config_rs12(args, world, rank, dev):
     ok = ok and torch.equal(par, st[:, k:]) and parity_rows_verified(coder, st)  # parity rows 0..3 all read
     enc_ms = sorted(a.elapsed_time(b) for a, b in enc_ev)[len(enc_ev) // 2]
     enc_gbs = B * (k + m) * L / (enc_ms * 1e-3) / 1e9
+    # each launch against a probe of its own stream mix (8 in / 4 out, 8 in / e out; no GF work)
+    mixes = {"encode": mix_ceiling([st[:, j] for j in range(k)], [par[:, r] for r in range(m)], Lc)}
+    if e in (1, 2, 4):
+        mixes["decode"] = mix_ceiling([st[:, j] for j in surv], [out[:, r] for r in range(e)], Lc)
+    torch.cuda.synchronize()
+    dec_k = {"ms": round(ms, 4), "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    enc_k = {"ms": round(enc_ms, 4), "GB/s": round(enc_gbs, 1), "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
+             "mix_probe": mixes["encode"], "frac_of_mix": round(mixes["encode"]["ms"] / enc_ms, 4)}
+    if "decode" in mixes:
+        dec_k.update(mix_probe=mixes["decode"], frac_of_mix=round(mixes["decode"]["ms"] / ms, 4))
     name = {1: "single", 2: "two", 3: "three", 4: "four"}[e]
     return {"metric": f"GiB/s device-resident RS(12,8) {name}-erasure decode, 256 KiB chunks",
-            "kernels": {f"decode_{e}erasure": {"ms": round(ms, 4), "GB/s": round(gbs, 1),
-                                            "frac": round(gbs / HBM_PEAK_GBS, 4)},
-                        "encode": {"ms": round(enc_ms, 4), "GB/s": round(enc_gbs, 1),
-                                   "frac": round(enc_gbs / HBM_PEAK_GBS, 4)}},
+            "kernels": {f"decode_{e}erasure": dec_k, "encode": enc_k},
             "value": round(world * args.steps * B * k * L / dt / GIB, 2), "unit": "GiB/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4), "host_submit_ms_per_step": round(submit, 4),
@@ -1027,9 +1037,23 @@ def config_hostpath(args, world, rank, dev):
         raise RuntimeError("--host-alloc pinned: elect_ec_host_alloc returned memory that is not page-locked")
     calls = max(4, args.steps // 2) * max(1, 4404020 // L // 8) * ndev
     fused = args.host_op == "encode_ex"
+    op = args.host_op
+    # decode: each caller rebuilds its unit 0 into a unit of its own; update: a new version of
+    # unit 1 per caller, applied in place to its parity (alternating old/new keeps the data valid)
+    extra = [host_array(L) for _ in range(T)] if op in ("decode", "update") else []
+    if op == "decode":
+        for t in range(T):
+            d, p = bufs[t]
+            coder.encode_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L)
+    if op == "update":
+        for t in range(T):
+            extra[t][:] = np.random.default_rng(10_000 + t).integers(0, 256, L, dtype=np.uint8)
+            d, p = bufs[t]
+            coder.encode_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L)
     content = [int(L / 1.05) - 64 * j for j in range(k)]  # SSTables just under codeLength/1.05
 
     errors = []
+    update_counts = [0] * T
 
     def worker(t, n):
         try:
@@ -1037,6 +1061,17 @@ def config_hostpath(args, world, rank, dev):
                 torch.cuda.set_device(dev)
             d, p = bufs[t]
             da, pa = [x.ctypes.data for x in d], [x.ctypes.data for x in p]
+            if op == "decode":
+                surv, out = [pa[0]] + da[1:], [extra[t].ctypes.data]
+                for _ in range(n):
+                    coder.decode_host(surv, [4, 1, 2, 3], [0], out, L)
+                return
+            if op == "update":
+                ver = [da[1], extra[t].ctypes.data]  # the current and the next version of unit 1
+                for i in range(n):
+                    coder.encode_update_host([ver[i % 2], ver[(i + 1) % 2]] + pa, 1, pa, L)
+                update_counts[t] += n
+                return
             for _ in range(n):
                 if fused:
                     coder.encode_ex_host(da, pa, L, data_lengths=content, hashed=True)
@@ -1069,7 +1104,17 @@ def config_hostpath(args, world, rank, dev):
     rebuilt = np.empty(L, np.uint8)
     coder.decode_host([p[0].ctypes.data] + [x.ctypes.data for x in d[1:]], [4, 1, 2, 3], [0],
                       [rebuilt.ctypes.data], L)
-    ok = bool(np.array_equal(rebuilt, d[0])) if not fused else True
+    ok = bool(np.array_equal(rebuilt, d[0])) if not fused and op != "update" else True
+    if op == "decode":  # every caller's last rebuilt unit is its unit 0
+        ok = ok and all(np.array_equal(extra[t], bufs[t][0][0]) for t in range(T))
+    if op == "update":  # each caller's parity now encodes its current version of unit 1
+        for t in range(T):
+            d, p = bufs[t]
+            cur = d[1] if update_counts[t] % 2 == 0 else extra[t]
+            units = [d[0], cur, d[2], d[3]]
+            ref = [np.empty(L, np.uint8) for _ in range(m)]
+            coder.encode_host([x.ctypes.data for x in units], [x.ctypes.data for x in ref], L)
+            ok = ok and all(np.array_equal(a, b) for a, b in zip(p, ref))
     if fused:  # self-check: the fused step's parity equals a plain encode of the zero-filled units
         from elect_amd.coder import java_bytebuffer_hash
         z = [np.concatenate([x[:n], np.zeros(L - n, np.uint8)]) for x, n in zip(d, content)]
@@ -1080,9 +1125,10 @@ def config_hostpath(args, world, rank, dev):
         ok = all(np.array_equal(a, b) for a, b in zip(p, ref)) and hs == [java_bytebuffer_hash(x) for x in ref]
     # every caller's last parity against the CPU oracle's restatement is in tests/; here each
     # caller's parity must at least equal caller 0's recomputation on its own data
-    op_name = "fused encode step (zero fill + encode + parity hashCode, elect_ec_encode_ex)" if fused else \
-        "encode"
-    data_gib = T * done * k * L / GIB
+    op_name = {"encode_ex": "fused encode step (zero fill + encode + parity hashCode, elect_ec_encode_ex)",
+               "decode": "single-erasure decode", "update": "parity update (encodeUpdate, in place)"}.get(op, "encode")
+    # data = the bytes each call reads: k units (encode, decode), old + new + m parity (update)
+    data_gib = T * done * (2 + m if op == "update" else k) * L / GIB
     stats = _lib.host_path_stats()
     core_ms = cpu * 1e3 / data_gib
     quota = host_cpu_info()["quota_cores"] or len(os.sched_getaffinity(0))

@@ -338,6 +338,14 @@ for step in "$@"; do
         run cfg_flows_64k 400 python bench.py --config flows || exit $?
         run cfg_hostpath_T64 400 python bench.py --config hostpath --threads 64 --host-seconds 2 || exit $?
         run cfg_hostpath_T64_pinned 400 python bench.py --config hostpath --threads 64 --host-seconds 2 --host-alloc pinned || exit $? ;;
+    hostops)  # the host path per JNI method at 64 callers, ELECT's codeLength: encode / decode / update / encode_ex,
+              # pageable and pool buffers
+        for o in ${HOST_OPS:-decode update encode encode_ex}; do for alloc in pageable pinned; do
+            run "hostop_${o}_${alloc}" 300 python bench.py --config hostpath --threads 64 --host-seconds 2 \
+                --host-op $o --host-alloc $alloc || exit $?
+        done; done ;;
+    rs12)  # configs[4] with each launch's stream-mix probe
+        for i in ${RS12_RUNS:-1 2}; do run "cfg_rs12_$i" 400 python bench.py --config rs12 || exit $?; done ;;
     padfill)  # padded encode vs content fill: where the time goes
         for f in 1.0 0.0 0.5 random; do
             run "bench_padded_fill_$f" 300 python bench.py --config padded --pad-fill $f || exit $?
