@@ -113,17 +113,29 @@ public:
             }
         }
         void* p = nullptr;
-        const hipError_t e = hipHostMalloc(&p, cls, hipHostMallocPortable);
-        bool pinned = e == hipSuccess && p;
-        if (!pinned) {
-            if (std::getenv("ELECT_EC_DEBUG"))
-                std::fprintf(stderr, "elect_ec_host_alloc: hipHostMalloc(%zu) failed: %s\n", cls, hipGetErrorString(e));
-            (void)hipGetLastError();
+        intptr_t delta = 0;  // device address - host address (the batches' kernels read the units there)
+        bool pinned = false;
+        if (kind() == kHsaLock) {  // A/B: ordinary memory locked for every agent (as the pageable path's units)
             p = std::aligned_alloc(4096, cls);
             if (!p) return nullptr;
+            void* ap = nullptr;
+            static const bool hsa = hsa_init() == HSA_STATUS_SUCCESS;  // once (reference counted)
+            pinned = hsa && hsa_amd_memory_lock(p, cls, nullptr, 0, &ap) == HSA_STATUS_SUCCESS;
+            if (pinned) delta = reinterpret_cast<intptr_t>(ap) - reinterpret_cast<intptr_t>(p);
+        } else {
+            const unsigned flags = hipHostMallocPortable | (kind() == kNonCoherent ? hipHostMallocNonCoherent : 0u) |
+                                   (kind() == kCoherent ? hipHostMallocCoherent : 0u);
+            const hipError_t e = hipHostMalloc(&p, cls, flags);
+            pinned = e == hipSuccess && p;
+            if (!pinned) {
+                if (std::getenv("ELECT_EC_DEBUG"))
+                    std::fprintf(stderr, "elect_ec_host_alloc: hipHostMalloc(%zu) failed: %s\n", cls, hipGetErrorString(e));
+                (void)hipGetLastError();
+                p = std::aligned_alloc(4096, cls);
+                if (!p) return nullptr;
+            }
         }
-        intptr_t delta = 0;  // device address - host address (the batches' kernels read the units there)
-        if (pinned) {
+        if (pinned && kind() != kHsaLock) {
             void* d = nullptr;
             if (hipHostGetDevicePointer(&d, p, 0) == hipSuccess)
                 delta = reinterpret_cast<intptr_t>(d) - reinterpret_cast<intptr_t>(p);
@@ -134,13 +146,41 @@ public:
             live_[reinterpret_cast<uintptr_t>(p)] = Block{cls, pinned, delta};
             if (pinned) delta_[p] = delta;
         } catch (...) {  // no record, no buffer: nothing leaks
-            if (pinned)
-                (void)hipHostFree(p);
-            else
-                std::free(p);
+            release_block(p, pinned);
             return nullptr;
         }
         return p;
+    }
+
+    // How page-locked blocks are made (ELECT_EC_POOL_ALLOC): aligned_alloc +
+    // hsa_amd_memory_lock for every agent ("hsalock", the default), or
+    // hipHostMalloc with the runtime's default coherence ("hip"), non-coherent
+    // ("nc") or coherent ("coherent").  The batches' gather / scatter kernels
+    // move 64 callers' pool units at 49.3-49.4 GiB/s from locked blocks against
+    // 46.9-47.7 from any hipHostMalloc kind (profiles/r05/pool_alloc_ab.txt).
+    // The library reaches pool units only through kernels at their device
+    // address (direct batches, zero-copy) or by CPU copies (the per-thread
+    // engine); round 4's per-piece hipMemcpyAsync A/B (ELECT_EC_DIRECT_MOVE=dma)
+    // wants "hip" blocks, which the HIP runtime knows as page-locked.
+    enum Kind { kHip, kNonCoherent, kCoherent, kHsaLock };
+    static Kind kind()
+    {
+        static const Kind k = [] {
+            const char* e = std::getenv("ELECT_EC_POOL_ALLOC");
+            const std::string v = e ? e : "";
+            return v == "hip" ? kHip : v == "nc" ? kNonCoherent : v == "coherent" ? kCoherent : kHsaLock;
+        }();
+        return k;
+    }
+
+    static void release_block(void* p, bool pinned)
+    {
+        if (pinned && kind() != kHsaLock) {
+            (void)hipHostFree(p);
+            return;
+        }
+        if (pinned) (void)hsa_amd_memory_unlock(p);
+        std::free(p);
     }
 
     bool free(void* p)
@@ -161,10 +201,7 @@ public:
                 }
             }
         }
-        if (b.pinned)
-            (void)hipHostFree(p);
-        else
-            std::free(p);
+        release_block(p, b.pinned);
         return true;
     }
 

@@ -344,6 +344,12 @@ for step in "$@"; do
             run "hostop_${o}_${alloc}" 300 python bench.py --config hostpath --threads 64 --host-seconds 2 \
                 --host-op $o --host-alloc $alloc || exit $?
         done; done ;;
+    poolalloc)  # page-locked pool blocks: hipHostMalloc default / non-coherent / coherent / aligned_alloc + HSA lock,
+                # 64 pool callers, interleaved
+        for i in 1 2; do for v in ${POOL_KINDS:-hip nc coherent hsalock}; do
+            ELECT_EC_POOL_ALLOC=$v run "poolalloc_${v}_$i" 300 python bench.py --config hostpath --threads 64 \
+                --host-seconds 2 --host-alloc pinned --host-op ${HOST_OP:-encode} || exit $?
+        done; done ;;
     rs12)  # configs[4] with each launch's stream-mix probe
         for i in ${RS12_RUNS:-1 2}; do run "cfg_rs12_$i" 400 python bench.py --config rs12 || exit $?; done ;;
     padfill)  # padded encode vs content fill: where the time goes
