@@ -690,6 +690,16 @@ inline bool cauchy_enabled()
     return on;
 }
 
+// ELECT_EC_CAUCHY_LDS=1: the structured form loads through LDS (LDS-DMA) in one-wave launches (A/B).
+inline bool cauchy_lds()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("ELECT_EC_CAUCHY_LDS");
+        return e && std::atoi(e) == 1;
+    }();
+    return on;
+}
+
 // Stage the byte-shuffle tables of a launch into LDS (8 dwords per coefficient).
 template <int K, int R>
 __device__ __forceinline__ void stage_tables(const gf::PermTable (&tab)[R][K], uint32_t* tl)
@@ -901,10 +911,13 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16u(const FastArgs<K, R> a)
 // tables of a group live in VGPRs), so 20 waves per CU; asking the allocator
 // for 6 / 7 / 8 waves per SIMD spilled 45 / 99 / 103 VGPRs, and the occupancy
 // sweep (profiles/r05/rs12_cauchy_ab.txt) is flat above 16 waves per CU.
-template <int K>
+// LDSDMA (A/B, ELECT_EC_CAUCHY_LDS=1): one-wave blocks load their columns
+// through LDS as gf_apply_x16u's LDS-DMA form does.
+template <int K, bool LDSDMA = false>
 __global__ __launch_bounds__(kBlock) void gf_apply_x16c(const FastArgs<K, 4> a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tl[4 * K * kTabStride];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[LDSDMA ? K * 1024 : 16];
     const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t first = __builtin_amdgcn_readfirstlane(idx);
     const uint32_t stripe = div_magic(first, a.magic, a.shift);
@@ -912,8 +925,15 @@ __global__ __launch_bounds__(kBlock) void gf_apply_x16c(const FastArgs<K, 4> a)
     stage_tables<K, 4>(a.tab, tl);
     if (first >= a.total) return;
     uint4 x[K];
+    if constexpr (LDSDMA) {
+        const uint8_t* src[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + static_cast<uint64_t>(stripe) * a.ss[j] + off);
+        for (int j = 0; j < K; ++j) src[j] = a.sp[j] + static_cast<uint64_t>(stripe) * a.ss[j] + off;
+        load_columns_via_lds<K>(src, stage, x);
+    } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = load_nt(a.sp[j] + static_cast<uint64_t>(stripe) * a.ss[j] + off);
+    }
     uint4 acc[4];
     gf_combine_cauchy4<K>(x, tl, acc);
 #pragma unroll
@@ -1303,7 +1323,11 @@ hipError_t launch_fast_kr(const ApplyParams& p, int r0, hipStream_t stream)
                     if (!launched && scalar_base && cauchy_enabled() && cauchy_blocks(p.coef, p.cols, r0, R)) {
                         FastArgs<K, R> ac = a;
                         cauchy_tables(p.coef, p.cols, r0, &ac.tab[0][0]);
-                        hipLaunchKernelGGL((gf_apply_x16c<K>), grid, dim3(sh.block), lds, stream, ac);
+                        if (sh.block == 64 && p.aligned16 && cauchy_lds())
+                            hipLaunchKernelGGL((gf_apply_x16c<K, true>), grid, dim3(sh.block), cap_lds(sh, kCoefs, K * 1024),
+                                               stream, ac);
+                        else
+                            hipLaunchKernelGGL((gf_apply_x16c<K>), grid, dim3(sh.block), lds, stream, ac);
                         launched = true;
                     }
                 }

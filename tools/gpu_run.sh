@@ -350,6 +350,12 @@ for step in "$@"; do
             ELECT_EC_POOL_ALLOC=$v run "poolalloc_${v}_$i" 300 python bench.py --config hostpath --threads 64 \
                 --host-seconds 2 --host-alloc pinned --host-op ${HOST_OP:-encode} || exit $?
         done; done ;;
+    cauchylds)  # RS(12,8) encode: the structured form loading through LDS (ELECT_EC_CAUCHY_LDS=1) vs into VGPRs, interleaved
+        for i in 1 2 3; do for v in 1 0; do
+            ELECT_EC_CAUCHY_LDS=$v run "cauchylds_${v}_$i" 300 python bench.py --config rs12 || exit $?
+        done; done ;;
+    repeats)  # the driver's bench command, back to back (run-to-run spread of the line)
+        for i in ${REPEAT_RUNS:-1 2 3}; do run "bench_driver_rep$i" 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $?; done ;;
     rs12)  # configs[4] with each launch's stream-mix probe
         for i in ${RS12_RUNS:-1 2}; do run "cfg_rs12_$i" 400 python bench.py --config rs12 || exit $?; done ;;
     padfill)  # padded encode vs content fill: where the time goes
