@@ -7,6 +7,7 @@
 #include <hsa/hsa_ext_amd.h>
 
 #include <emmintrin.h>
+#include <pthread.h>
 
 #include <algorithm>
 #include <atomic>
@@ -32,16 +33,17 @@ namespace {
 
 using kern::ApplyParams;
 
-// Host threads wait for the device with hipStreamSynchronize, and the batcher's
-// completions come from a host-function callback (hipLaunchHostFunc).  Round 4
-// measured the alternative the round-3 review proposed: events created with
-// hipEventBlockingSync and a completion thread of the batcher's own sleeping on
-// them (profiles/r04/hostwait_ab.txt, host_direct_ab.txt; 2 interleaved rounds,
-// ELECT's codeLength).  It saved no CPU and lost throughput everywhere: 64
-// callers on pageable buffers 48.6-49.3 -> 42.7-43.0 GiB/s, on page-locked
-// buffers 45.3 -> 39.5 GiB/s at 48 -> 58 core-ms per GiB.  On pageable buffers
-// the CPU goes to the staging copies; page-locked coding buffers remove those
-// (PinnedPool below, 4x less CPU per GiB).
+// Waiting for the device.  Every waiting primitive of this HIP runtime spins a
+// core while the work it waits for runs (hipStreamSynchronize, hipEventSynchronize
+// also on hipEventBlockingSync events, and the runtime thread that runs
+// hipLaunchHostFunc callbacks; tools/tune/spin_probe.cpp, profiles/r05/
+// spin_probe.txt).  So the batcher's completions come from a poller thread per
+// device that queries events and sleeps in between (Batcher::wait_mode: 35 -> 17
+// core-ms per GiB at 64 callers on pageable units, 28 -> 9 on pool units, the
+// same GiB/s; profiles/r05/completion_poll_ab.txt), and the per-thread engine
+// waits with wait_sleeping.  (Round 4's completion thread sleeping on
+// hipEventBlockingSync events saved no CPU for that reason, and lost throughput:
+// profiles/r04/hostwait_ab.txt.)
 
 // Host copies into and out of the pinned staging memory, with non-temporal
 // (streaming) stores: the data is not read again by this CPU (the DMA engine
@@ -775,6 +777,7 @@ private:
 
     void helper()
     {
+        pthread_setname_np(pthread_self(), "ec-copy");
         uint64_t seen = 0;
         std::unique_lock<std::mutex> lock(mu_);
         for (;;) {
@@ -814,6 +817,18 @@ void run_copies(const std::vector<CopyJob>& jobs, bool lone)
     _mm_sfence();  // the streamed stores are visible before the data is handed on
 }
 
+// Waits for ev without spinning a core: this HIP runtime's own waits spin for as
+// long as the work they wait for runs (Batcher::wait_mode); hipEventQuery with
+// sleeps from 2 up to 50 us costs ~2 % of a core instead.
+hipError_t wait_sleeping(hipEvent_t ev)
+{
+    for (unsigned us = 2;; us = std::min(us * 2, 50u)) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        std::this_thread::sleep_for(std::chrono::microseconds(us));
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Host-memory path: per-thread, per-device staging engine.
 // Input chunks are copied into pinned buffers, sent H2D, coded, returned D2H
@@ -830,6 +845,7 @@ public:
     {
         for (int s = 0; s < kSlots; ++s) {
             if (stream_[s]) (void)hipStreamDestroy(stream_[s]);
+            if (ev_[s]) (void)hipEventDestroy(ev_[s]);
             if (pin_in_[s]) (void)hipHostFree(pin_in_[s]);
             if (pin_out_[s]) (void)hipHostFree(pin_out_[s]);
             if (d_in_[s]) (void)hipFree(d_in_[s]);
@@ -857,7 +873,7 @@ public:
         for (size_t c = 0; c < nchunks + kSlots; ++c) {
             const int s = static_cast<int>(c % kSlots);
             if (busy[s]) {  // retire the chunk that used this slot
-                const hipError_t e = hipStreamSynchronize(stream_[s]);
+                const hipError_t e = wait_sleeping(ev_[s]);
                 if (e != hipSuccess) return map_hip(e);
                 const size_t o = pending[s] * step;
                 const size_t n = std::min(step, len - o);
@@ -888,6 +904,7 @@ public:
             if (e == hipSuccess) e = launch(op, s, pitch, n, op.lens ? valid : nullptr, o);
             if (e == hipSuccess)
                 e = hipMemcpyAsync(pin_out_[s], d_out_[s], op.rows * pitch, hipMemcpyDeviceToHost, stream_[s]);
+            if (e == hipSuccess) e = hipEventRecord(ev_[s], stream_[s]);
             if (e != hipSuccess) {
                 (void)hipStreamSynchronize(stream_[0]);
                 (void)hipStreamSynchronize(stream_[1]);
@@ -932,7 +949,8 @@ private:
     {
         if (!stream_[0]) {
             for (int s = 0; s < kSlots; ++s) {
-                const hipError_t e = hipStreamCreateWithFlags(&stream_[s], hipStreamNonBlocking);
+                hipError_t e = hipStreamCreateWithFlags(&stream_[s], hipStreamNonBlocking);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&ev_[s], hipEventDisableTiming);
                 if (e != hipSuccess) return map_hip(e);
             }
             hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_hash_), kern::kMaxRows * sizeof(int32_t));
@@ -975,6 +993,7 @@ private:
 
     [[maybe_unused]] int dev_;
     hipStream_t stream_[kSlots] = {};
+    hipEvent_t ev_[kSlots] = {};  // behind each slot's D2H (wait_sleeping)
     uint8_t* pin_in_[kSlots] = {};
     uint8_t* pin_out_[kSlots] = {};
     uint8_t* d_in_[kSlots] = {};
@@ -1164,6 +1183,7 @@ public:
             }
             try {
                 std::thread(&Batcher::worker, this).detach();  // lives as long as the process
+                if (wait_mode() == kWaitPoll) std::thread(&Batcher::poller, this).detach();
             } catch (...) {  // no dispatcher: the per-thread engine serves every call
                 release();
                 init_failed_ = true;
@@ -1319,8 +1339,10 @@ private:
         std::condition_variable done;  // this batch's callers wait here for kDone
         hipStream_t stream = nullptr;
         hipEvent_t h2d_done = nullptr;
+        hipEvent_t done_ev = nullptr;  // recorded behind the batch's last operation (completion by polling)
         hsa_signal_t sig{};  // counts a direct batch's outstanding HSA copies (ELECT_EC_DIRECT_MOVE=sdma)
-        bool h2d_landed = false;  // on_h2d ran for the batch in flight (under the owner's mu_)
+        bool h2d_landed = false;  // the batch in flight has its inputs on the device (under the owner's mu_)
+        bool issued = false;      // ... and all of its work is enqueued, events recorded (poll mode)
 
         Shape shape() const
         {
@@ -1382,6 +1404,7 @@ private:
             }();
             if (e == hipSuccess)
                 e = hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming | (blocking ? hipEventBlockingSync : 0));
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming);
             // device first: an arena too large for the device fails there, before any host pinning
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_in), arena);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_out), arena);
@@ -1436,6 +1459,7 @@ private:
         for (Slab& s : active()) {
             if (s.stream) (void)hipStreamDestroy(s.stream);
             if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
+            if (s.done_ev) (void)hipEventDestroy(s.done_ev);
             for (uint8_t* h : {s.pin_in, s.pin_out})
                 if (h) (void)hipHostFree(h);
             for (void* h : {static_cast<void*>(s.pin_lens), static_cast<void*>(s.pin_hash), static_cast<void*>(s.pieces)})
@@ -1445,6 +1469,7 @@ private:
                 if (d) (void)hipFree(d);
             s.stream = nullptr;
             s.h2d_done = nullptr;
+            s.done_ev = nullptr;
             s.pin_in = s.pin_out = s.d_in = s.d_out = nullptr;
             s.pin_lens = s.d_lens = nullptr;
             s.pin_hash = s.d_hash = nullptr;
@@ -1463,6 +1488,7 @@ private:
     // how long an idle device waits for more callers; 0 = never wait.
     void worker()
     {
+        pthread_setname_np(pthread_self(), ("ec-dispatch" + std::to_string(dev_)).c_str());
         (void)hipSetDevice(dev_);
         Slab* prev = nullptr;
         std::unique_lock<std::mutex> lock(mu_);
@@ -1475,7 +1501,7 @@ private:
                 return s != nullptr;
             });
             if (prev && prev->state == Slab::kInFlight) {  // wait for its H2D only
-                if (h2d_by_callback()) {  // asleep until prev's on_h2d (or its end)
+                if (wait_mode() != kWaitEvent) {  // asleep until the poller / on_h2d sees prev's inputs land
                     cv_worker_.wait(lock, [&] { return prev->h2d_landed || prev->state != Slab::kInFlight; });
                 } else {
                     hipEvent_t ev = prev->h2d_done;
@@ -1507,9 +1533,14 @@ private:
             const uint64_t t0 = thread_cpu_ns();
             const hipError_t e = issue(*s, shape, n, slots_);
             g_issue_cpu_ns.fetch_add(thread_cpu_ns() - t0);
-            if (e != hipSuccess) (void)hipStreamSynchronize(s->stream);  // no callback was queued
+            if (e != hipSuccess) (void)hipStreamSynchronize(s->stream);  // no completion was queued
             lock.lock();
-            if (e != hipSuccess) finish(s, map_hip(e));
+            if (e != hipSuccess) {
+                finish(s, map_hip(e));
+            } else if (wait_mode() == kWaitPoll) {
+                s->issued = true;
+                cv_poll_.notify_one();
+            }
             prev = s;
         }
     }
@@ -1614,7 +1645,7 @@ private:
             e = hipMemcpyAsync(s.d_lens, s.pin_lens, static_cast<size_t>(n) * sh.cols * sizeof(uint32_t),
                                hipMemcpyHostToDevice, s.stream);
         if (e == hipSuccess) e = hipEventRecord(s.h2d_done, s.stream);
-        if (e == hipSuccess && h2d_by_callback()) e = hipLaunchHostFunc(s.stream, &Batcher::on_h2d, &s);
+        if (e == hipSuccess && wait_mode() == kWaitCallback) e = hipLaunchHostFunc(s.stream, &Batcher::on_h2d, &s);
         if (e == hipSuccess) {
             // coding stripes: the slots' tiles in order (untiled: the slots)
             ApplyParams p;
@@ -1665,7 +1696,8 @@ private:
         if (e == hipSuccess && sh.hashed)
             e = hipMemcpyAsync(s.pin_hash, s.d_hash, static_cast<size_t>(n) * sh.rows * sizeof(int32_t),
                                hipMemcpyDeviceToHost, s.stream);
-        if (e == hipSuccess) e = hipLaunchHostFunc(s.stream, &Batcher::on_done, &s);
+        if (e == hipSuccess)
+            e = wait_mode() == kWaitPoll ? hipEventRecord(s.done_ev, s.stream) : hipLaunchHostFunc(s.stream, &Batcher::on_done, &s);
         return e;
     }
 
@@ -1701,20 +1733,82 @@ private:
         }
     };
 
-    // The dispatcher's wait for a batch's inputs to land (self-clocking): a host
-    // callback behind the H2D wakes it (the default), or it polls the event
-    // (ELECT_EC_DISPATCH_WAIT=event): hipEventSynchronize spins a core for the
-    // whole H2D, ~20 ms a batch at 64 callers (round 5, 64 callers, 2 runs each:
-    // pageable units 52.8-54.3 -> 34.1-37.1 core-ms per GiB, pool units
-    // 45.6-46.0 -> 26.7-28.3, staged 195-223 -> 211-222, the same GiB/s;
-    // profiles/r05/hostpath_register_ab.txt E).
-    static bool h2d_by_callback()
+    // How the dispatcher learns that a batch's inputs have landed (self-clocking)
+    // and the callers that their batch is done (ELECT_EC_DISPATCH_WAIT):
+    //  - poll (the default): a poller thread per device queries the batches'
+    //    events (hipEventQuery) and sleeps ELECT_EC_POLL_US (default 25) between
+    //    rounds;
+    //  - callback: host-function callbacks behind the H2D and behind the batch
+    //    (hipLaunchHostFunc);
+    //  - event: the dispatcher waits in hipEventSynchronize, completions by callback.
+    // Every waiting primitive of this HIP runtime spins a core for as long as the
+    // device work it waits for runs: hipStreamSynchronize, hipEventSynchronize
+    // (hipEventBlockingSync events too) 94 % of a core each behind 5 ms kernels,
+    // the runtime's host-function thread 96 % (tools/tune/spin_probe.cpp,
+    // profiles/r05/spin_probe.txt), where hipEventQuery every 50 us costs 2 %.  At
+    // 64 callers the callback thread alone was 19-20 core-ms per GiB, the largest
+    // single cost of the host path (tools/hostpath_cbench per-thread CPU).  The
+    // event mode first spun the dispatcher too (round 5 before callbacks: 53
+    // against 35 core-ms per GiB, hostpath_register_ab.txt E).
+    enum WaitMode { kWaitPoll, kWaitCallback, kWaitEvent };
+    static WaitMode wait_mode()
     {
-        static const bool c = [] {
+        static const WaitMode m = [] {
             const char* e = std::getenv("ELECT_EC_DISPATCH_WAIT");
-            return !(e && std::string(e) == "event");
+            const std::string v = e ? e : "";
+            return v == "event" ? kWaitEvent : v == "callback" ? kWaitCallback : kWaitPoll;
         }();
-        return c;
+        return m;
+    }
+    static unsigned poll_us()
+    {
+        static const unsigned u = [] {
+            const char* e = std::getenv("ELECT_EC_POLL_US");
+            return e ? static_cast<unsigned>(std::max(1, std::atoi(e))) : 25u;
+        }();
+        return u;
+    }
+
+    // Poll mode: marks in-flight batches' inputs landed (waking the dispatcher)
+    // and finishes completed batches (waking their callers).  Only this thread
+    // finishes an issued batch, so a batch it saw issued stays in flight until
+    // it finishes it.
+    void poller()
+    {
+        pthread_setname_np(pthread_self(), ("ec-poll" + std::to_string(dev_)).c_str());
+        (void)hipSetDevice(dev_);
+        std::unique_lock<std::mutex> lock(mu_);
+        for (;;) {
+            cv_poll_.wait(lock, [&] {
+                for (Slab& x : active())
+                    if (x.state == Slab::kInFlight && x.issued) return true;
+                return false;
+            });
+            for (Slab& x : active()) {
+                if (x.state != Slab::kInFlight || !x.issued) continue;
+                const bool landed = x.h2d_landed;
+                lock.unlock();  // (a slab's events never change after init)
+                // the batch cannot be done before its inputs have landed
+                const hipError_t eh = landed ? hipSuccess : hipEventQuery(x.h2d_done);
+                const hipError_t ed = eh == hipSuccess ? hipEventQuery(x.done_ev) : hipErrorNotReady;
+                lock.lock();
+                if (!landed && eh != hipErrorNotReady) {
+                    x.h2d_landed = true;
+                    cv_worker_.notify_one();
+                }
+                if (eh != hipSuccess && eh != hipErrorNotReady) {  // a failed batch is done, with its error
+                    (void)hipGetLastError();
+                    finish(&x, map_hip(eh));
+                    continue;
+                }
+                if (ed == hipErrorNotReady) continue;
+                if (ed != hipSuccess) (void)hipGetLastError();
+                finish(&x, ed == hipSuccess ? ELECT_EC_OK : map_hip(ed));
+            }
+            lock.unlock();
+            std::this_thread::sleep_for(std::chrono::microseconds(poll_us()));
+            lock.lock();
+        }
     }
 
     static void on_h2d(void* arg)  // HIP host-function callback: no HIP calls in here
@@ -1735,6 +1829,7 @@ private:
     void finish(Slab* s, int status)  // mu_ held
     {
         s->status = status;
+        s->issued = false;
         if (s->readers == 0) {
             s->state = Slab::kFree;
             cv_slot_.notify_all();
@@ -1751,6 +1846,7 @@ private:
     // every reservation: O(callers^2) wake-ups per batch at 64 callers).
     std::mutex mu_;
     std::condition_variable cv_worker_;  // the dispatcher
+    std::condition_variable cv_poll_;    // the poller (poll mode), while no batch is in flight
     DirectSlots slots_;                  // the dispatcher's copy of a direct batch's slots (its thread only)
     std::condition_variable cv_slot_;    // callers waiting for an arena to reserve in
     bool started_ = false;

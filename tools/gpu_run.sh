@@ -356,6 +356,28 @@ for step in "$@"; do
         done; done ;;
     repeats)  # the driver's bench command, back to back (run-to-run spread of the line)
         for i in ${REPEAT_RUNS:-1 2 3}; do run "bench_driver_rep$i" 600 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $?; done ;;
+    cthreads)  # per-thread CPU of the host path from C++ callers (tools/hostpath_cbench, built here): pageable and pool
+        for i in 1 2; do for pool in 0 1; do
+            run "cthreads_pool${pool}_$i" 120 tools/hostpath_cbench 64 3 4404020 4 $pool || exit $?
+        done; done ;;
+    spin)  # which runtime thread burns a core, by what the process queues (tools/tune/spin_probe.cpp, built here)
+        for m in ${SPIN_MODES:-idle kernels hostfunc hostfunc_burst event blocking hsa_lock longk_hostfunc longk_sync}; do
+            run "spin_$m" 60 tools/tune/spin_probe $m || exit $?
+        done ;;
+    waitab)  # batch completion: poller thread (default, ELECT_EC_POLL_US 25 / 50) vs host-function callbacks, interleaved;
+             # C++ callers with per-thread CPU, then the Python bench, pageable and pool units
+        for i in 1 2; do for w in poll25 poll50 callback; do
+            mode=${w%%[0-9]*}; us=${w#poll}; [ "$mode" = poll ] || us=25
+            for pool in 0 1; do
+                ELECT_EC_DISPATCH_WAIT=$mode ELECT_EC_POLL_US=$us run "waitab_${w}_c${pool}_$i" 120 tools/hostpath_cbench 64 3 4404020 4 $pool || exit $?
+            done
+            ELECT_EC_DISPATCH_WAIT=$mode ELECT_EC_POLL_US=$us run "waitab_${w}_py_$i" 300 python bench.py --config hostpath \
+                --threads 64 --host-seconds 2 || exit $?
+        done; done ;;
+    hostcallers)  # pageable encode at 8 / 16 / 32 / 64 callers on one device
+        for T in ${CALLERS:-8 16 32 64}; do
+            run "hostcallers_T$T" 300 python bench.py --config hostpath --threads $T --host-seconds 2 || exit $?
+        done ;;
     rs12)  # configs[4] with each launch's stream-mix probe
         for i in ${RS12_RUNS:-1 2}; do run "cfg_rs12_$i" 400 python bench.py --config rs12 || exit $?; done ;;
     padfill)  # padded encode vs content fill: where the time goes
