@@ -1967,6 +1967,7 @@ struct ZeroCopy {
     // coding pools retire threads).
     struct ThreadStreams {
         hipStream_t stream[kMaxDevices] = {};
+        hipEvent_t done[kMaxDevices] = {};  // the call's end (wait_sleeping)
         ~ThreadStreams()
         {
             for (int d = 0; d < kMaxDevices; ++d) {
@@ -1974,6 +1975,7 @@ struct ZeroCopy {
                 int prev = 0;
                 const bool other = hipGetDevice(&prev) == hipSuccess && prev != d && hipSetDevice(d) == hipSuccess;
                 (void)hipStreamDestroy(stream[d]);
+                if (done[d]) (void)hipEventDestroy(done[d]);
                 if (other) (void)hipSetDevice(prev);
             }
         }
@@ -1990,6 +1992,10 @@ struct ZeroCopy {
             ts.stream[dev] = nullptr;
             (void)hipGetLastError();
             return kFallback;
+        }
+        if (!ts.done[dev] && hipEventCreateWithFlags(&ts.done[dev], hipEventDisableTiming) != hipSuccess) {
+            ts.done[dev] = nullptr;  // (the call then waits in hipStreamSynchronize)
+            (void)hipGetLastError();
         }
         hipStream_t stream = ts.stream[dev];
         // through the registry: a range sharing a page with any live registration
@@ -2044,7 +2050,8 @@ struct ZeroCopy {
                 hipError_t e = kern::launch_apply(p, stream);
                 // Whatever was enqueued finishes before the pages are unregistered,
                 // also when a later launch of the call failed.
-                const hipError_t w = hipStreamSynchronize(stream);
+                hipError_t w = ts.done[dev] ? hipEventRecord(ts.done[dev], stream) : hipErrorInvalidHandle;
+                w = w == hipSuccess ? wait_sleeping(ts.done[dev]) : hipStreamSynchronize(stream);
                 if (e == hipSuccess) e = w;
                 // A shape the single launch does not take (hipErrorInvalidValue is
                 // returned before the kernels run: a wide padded update past 2^31
