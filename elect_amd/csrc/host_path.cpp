@@ -596,6 +596,19 @@ bool direct_h2d_sdma()
     return k;
 }
 
+// Bytes per gather / scatter piece (ELECT_EC_PIECE_KB, 4..64, default 64): the
+// copy kernels' blocks take pieces round robin, so a launch ends with a tail of
+// at most one piece per block.
+size_t piece_bytes()
+{
+    static const size_t b = [] {
+        const char* e = std::getenv("ELECT_EC_PIECE_KB");
+        const int kb = e ? std::atoi(e) : 64;
+        return static_cast<size_t>(std::min(64, std::max(4, kb))) << 10;
+    }();
+    return b;
+}
+
 // A CPU agent (the source side of host-to-device HSA copies).
 bool hsa_cpu_agent(hsa_agent_t* out)
 {
@@ -1415,7 +1428,7 @@ private:
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_lens), meta);
             if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_hash), meta, hipHostMallocDefault);
             // gather: <= one piece per 64 KiB of the arena plus 3 per unit; the scatter as many
-            s.max_pieces = 2 * (arena / kern::kMaxPieceBytes + 3 * kMaxDirectSlots * std::max(kern::kMaxCols, kern::kMaxRows));
+            s.max_pieces = 2 * (arena / piece_bytes() + 3 * kMaxDirectSlots * std::max(kern::kMaxCols, kern::kMaxRows));
             if (e == hipSuccess)
                 e = hipHostMalloc(reinterpret_cast<void**>(&s.pieces), s.max_pieces * sizeof(kern::CopyPiece),
                                   hipHostMallocDefault);
@@ -1581,13 +1594,13 @@ private:
             }
             bool copy_failed = false;
             auto piece = [&](const uint8_t* from, uint8_t* to, size_t bytes) {
-                for (size_t o = 0; o < bytes; o += kern::kMaxPieceBytes) {
+                for (size_t o = 0; o < bytes; o += piece_bytes()) {
                     if (np == s.max_pieces) {
                         overflow = true;
                         return;
                     }
                     s.pieces[np++] = kern::CopyPiece{from + o, to + o,
-                                                     static_cast<uint32_t>(std::min<size_t>(kern::kMaxPieceBytes, bytes - o)), 0};
+                                                     static_cast<uint32_t>(std::min<size_t>(piece_bytes(), bytes - o)), 0};
                 }
             };
             for (int q = 0; q < n; ++q)

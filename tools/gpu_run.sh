@@ -164,7 +164,7 @@ for step in "$@"; do
         done; done; done; done ;;
     hostprof)  # kernel trace of the pageable host path at 64 callers (gather / code / scatter durations)
         run hostprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/hostprof_$TAG -o run \
-            -- python3 bench.py --config hostpath --threads 64 --host-seconds 2 --steps 8 || exit $? ;;
+            -- python3 bench.py --config hostpath --threads ${T:-64} --host-seconds 2 --steps 8 || exit $? ;;
     hostsweep) run hostsweep 600 python tools/tune/host_sweep.py || exit $? ;;
     copysizes) run copysizes 600 python tools/tune/host_sweep.py copysizes || exit $? ;;
     staged)
@@ -376,8 +376,19 @@ for step in "$@"; do
         done; done ;;
     hostcallers)  # pageable encode at 8 / 16 / 32 / 64 callers on one device
         for T in ${CALLERS:-8 16 32 64}; do
-            run "hostcallers_T$T" 300 python bench.py --config hostpath --threads $T --host-seconds 2 || exit $?
+            run "hostcallers_T$T" 300 python bench.py --config hostpath --threads $T --host-seconds ${HOST_S:-2} || exit $?
         done ;;
+    lowconc)  # 8 callers on one device (64 over 8 GPUs): arenas x arena size x poll interval, interleaved, 3 s runs
+        IFS=';' read -ra CFGS <<< "${LOW_CFGS:-3 256 25;4 256 25;3 54 25;4 54 25;3 256 5}"
+        for i in 1 2; do for c in "${CFGS[@]}"; do
+            set -- $c
+            ELECT_EC_BATCH_SLABS=$1 ELECT_EC_BATCH_ARENA_MB=$2 ELECT_EC_POLL_US=$3 run "lowconc_s$1_a$2_p$3_T${T:-8}_$i" 300 \
+                python bench.py --config hostpath --threads ${T:-8} --host-seconds 3 || exit $?
+        done; done ;;
+    piecekb)  # gather / scatter piece size (ELECT_EC_PIECE_KB) at 8 and 64 callers, interleaved, 3 s runs
+        for i in 1 2; do for kb in ${PIECE_KBS:-64 32 16 8}; do for T in ${T_LIST:-8 64}; do
+            ELECT_EC_PIECE_KB=$kb run "piecekb_${kb}_T${T}_$i" 300 python bench.py --config hostpath --threads $T --host-seconds 3 || exit $?
+        done; done; done ;;
     rs12)  # configs[4] with each launch's stream-mix probe
         for i in ${RS12_RUNS:-1 2}; do run "cfg_rs12_$i" 400 python bench.py --config rs12 || exit $?; done ;;
     padfill)  # padded encode vs content fill: where the time goes
