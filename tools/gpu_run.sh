@@ -386,7 +386,7 @@ for step in "$@"; do
                 python bench.py --config hostpath --threads ${T:-8} --host-seconds 3 || exit $?
         done; done ;;
     piecekb)  # gather / scatter piece size (ELECT_EC_PIECE_KB) at 8 and 64 callers, interleaved, 3 s runs
-        for i in 1 2; do for kb in ${PIECE_KBS:-64 32 16 8}; do for T in ${T_LIST:-8 64}; do
+        for i in ${PIECE_RUNS:-1 2}; do for kb in ${PIECE_KBS:-64 32 16 8}; do for T in ${T_LIST:-8 64}; do
             ELECT_EC_PIECE_KB=$kb run "piecekb_${kb}_T${T}_$i" 300 python bench.py --config hostpath --threads $T --host-seconds 3 || exit $?
         done; done; done ;;
     rs12)  # configs[4] with each launch's stream-mix probe
