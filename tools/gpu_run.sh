@@ -389,6 +389,12 @@ for step in "$@"; do
         for i in ${PIECE_RUNS:-1 2}; do for kb in ${PIECE_KBS:-64 32 16 8}; do for T in ${T_LIST:-8 64}; do
             ELECT_EC_PIECE_KB=$kb run "piecekb_${kb}_T${T}_$i" 300 python bench.py --config hostpath --threads $T --host-seconds 3 || exit $?
         done; done; done ;;
+    zcwaves)  # a lone caller: zero-copy launches capped at W waves per CU (ELECT_EC_ZC_WAVES) vs the batched path
+        for i in 1 2; do for w in ${ZC_WAVES:-off 0 1 2 4 8}; do
+            if [ $w = off ]; then z=0; else z=1; fi
+            ELECT_EC_ZEROCOPY=$z ELECT_EC_ZC_WAVES=${w/off/0} run "zcwaves_${w}_T${T:-1}_$i" 300 python bench.py --config hostpath \
+                --threads ${T:-1} --host-seconds 2 || exit $?
+        done; done ;;
     rs12)  # configs[4] with each launch's stream-mix probe
         for i in ${RS12_RUNS:-1 2}; do run "cfg_rs12_$i" 400 python bench.py --config rs12 || exit $?; done ;;
     padfill)  # padded encode vs content fill: where the time goes
