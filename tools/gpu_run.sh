@@ -395,6 +395,10 @@ for step in "$@"; do
             ELECT_EC_ZEROCOPY=$z ELECT_EC_ZC_WAVES=${w/off/0} run "zcwaves_${w}_T${T:-1}_$i" 300 python bench.py --config hostpath \
                 --threads ${T:-1} --host-seconds 2 || exit $?
         done; done ;;
+    gateab)  # dispatch gate (a batch waits for the previous batch's inputs to land) on / off, C++ callers, interleaved
+        for i in 1 2; do for g in 1 0; do for T in ${T_LIST:-8 16 64}; do
+            ELECT_EC_DISPATCH_GATE=$g run "gateab_g${g}_T${T}_$i" 120 tools/hostpath_cbench $T 3 4404020 4 0 || exit $?
+        done; done; done ;;
     rs12)  # configs[4] with each launch's stream-mix probe
         for i in ${RS12_RUNS:-1 2}; do run "cfg_rs12_$i" 400 python bench.py --config rs12 || exit $?; done ;;
     padfill)  # padded encode vs content fill: where the time goes
