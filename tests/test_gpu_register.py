@@ -118,9 +118,13 @@ print("BAD " + "; ".join(errors[:6]) if errors else "OK", json.dumps(stats))
 """
 
 
-def test_registered_units_back_to_back_then_device_work():
+# The batcher's completion mechanisms (Batcher::wait_mode): the poller (default),
+# host-function callbacks, and the dispatcher in hipEventSynchronize (A/B modes).
+@pytest.mark.parametrize("wait", ["poll", "callback", "event"])
+def test_registered_units_back_to_back_then_device_work(wait):
     code = SCRIPT.replace("ROOT", repr(ROOT))
-    env = dict(os.environ, ELECT_EC_REGISTER="1", ELECT_EC_REGISTER_SLOTS="4", ELECT_EC_ZEROCOPY="0")
+    env = dict(os.environ, ELECT_EC_REGISTER="1", ELECT_EC_REGISTER_SLOTS="4", ELECT_EC_ZEROCOPY="0",
+               ELECT_EC_DISPATCH_WAIT=wait)
     env.pop("ELECT_EC_DIRECT_MOVE", None)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0 and r.stdout.strip().startswith("OK"), r.stdout[-3000:] + r.stderr[-3000:]
