@@ -399,6 +399,11 @@ for step in "$@"; do
         for i in 1 2; do for g in 1 0; do for T in ${T_LIST:-8 16 64}; do
             ELECT_EC_DISPATCH_GATE=$g run "gateab_g${g}_T${T}_$i" 120 tools/hostpath_cbench $T 3 4404020 4 0 || exit $?
         done; done; done ;;
+    bitslice)  # RS(12,8) encode: bitsliced (tools/tune/bitslice_probe.hip, built here) vs the product, bytes compared,
+               # then SQ counters of both kernels in one pass (VALU instructions, waves, GUI-active cycles for the clock)
+        run bitslice 120 tools/tune/bitslice_probe 20 || exit $?
+        run bitslice_pmc 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --kernel-trace \
+            --output-format csv -d $OUT/bitslice_pmc -o run -- tools/tune/bitslice_probe 5 || exit $? ;;
     rs12)  # configs[4] with each launch's stream-mix probe
         for i in ${RS12_RUNS:-1 2}; do run "cfg_rs12_$i" 400 python bench.py --config rs12 || exit $?; done ;;
     padfill)  # padded encode vs content fill: where the time goes
