@@ -147,8 +147,8 @@ int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes);
  * interior pages; its partial end pages are staged), out[6] such attempts that
  * took the staged path instead (no free registration slot, ELECT_EC_REGISTER_SLOTS,
  * or a range refused because it shares a page with a live registration of
- * another extent), out[7] hipHostUnregister failures (0 unless the runtime's
- * registrations were disturbed by another party), out[8..10] CPU time in ns
+ * another extent), out[7] unlock failures (hsa_amd_memory_unlock; 0 unless the
+ * runtime's locks were disturbed by another party), out[8..10] CPU time in ns
  * spent registering, unregistering, and issuing batches in the dispatcher
  * threads.  Writes min(n, 11) entries; returns the count. */
 int elect_ec_host_path_stats(uint64_t* out, int n);
@@ -164,7 +164,11 @@ int elect_ec_host_path_stats(uint64_t* out, int n);
  * and allocating one size per stripe reuses the same page-locked memory.
  * When page-locked memory is unavailable the buffer is ordinary memory and
  * calls on it take the staged path; *out is NULL only when no memory at all
- * could be had (ELECT_EC_ENOMEM).  Usable from any thread; free with
+ * could be had (ELECT_EC_ENOMEM).  The blocks are ordinary memory locked with
+ * hsa_amd_memory_lock for every GPU (ELECT_EC_POOL_ALLOC=hip: hipHostMalloc
+ * instead), so the HIP runtime does not list them as its own pinned memory:
+ * pass them to this library's calls, not to hipHostGetDevicePointer.  Usable
+ * from any thread; free with
  * elect_ec_host_free (EINVAL for a pointer not from elect_ec_host_alloc). */
 int elect_ec_host_alloc(size_t bytes, void** out);
 int elect_ec_host_free(void* ptr);
