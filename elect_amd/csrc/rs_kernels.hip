@@ -517,11 +517,13 @@ hipError_t launch_copy_pieces(const CopyPiece* pieces, uint32_t n, hipStream_t s
     (void)hipGetLastError();
     if (n == 0) return hipSuccess;
     if (n > 0x7FFFFFFFu) return hipErrorInvalidValue;
-    // ELECT_EC_COPY_VARIANT (A/B): 0 plain loads/stores, 4 in flight (default); 1 non-temporal, 4 in
-    // flight; 2 plain, one at a time; 3 non-temporal, one at a time
+    // ELECT_EC_COPY_VARIANT (A/B): 0 plain loads/stores, 4 in flight; 1 non-temporal, 4 in flight;
+    // 2 plain, one at a time (the default since the completion poller: 64 callers 49.55-49.66
+    // against 48.80-48.96 GiB/s, 8 callers 42.9-44.0 against 42.3-43.3, 3 interleaved runs,
+    // profiles/r05/hostpath_low_concurrency.txt); 3 non-temporal, one at a time
     static const int variant = [] {
         const char* e = std::getenv("ELECT_EC_COPY_VARIANT");
-        return e ? std::atoi(e) : 0;
+        return e ? std::atoi(e) : 2;
     }();
     // Few blocks (ELECT_EC_COPY_BLOCKS, default 128, half a block per CU): the copies wait on
     // PCIe, and a full-chip grid of them held the coding launches of other batches off the CUs

@@ -404,6 +404,11 @@ for step in "$@"; do
         run bitslice 120 tools/tune/bitslice_probe 20 || exit $?
         run bitslice_pmc 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --kernel-trace \
             --output-format csv -d $OUT/bitslice_pmc -o run -- tools/tune/bitslice_probe 5 || exit $? ;;
+    lowcopy)  # 8 callers: copy-kernel grid cap x variant (ELECT_EC_COPY_BLOCKS, ELECT_EC_COPY_VARIANT), interleaved
+        for i in 1 2; do for cb in ${LOW_BLOCKS:-64 128 256 512}; do for v in ${LOW_VARIANTS:-0 2}; do
+            ELECT_EC_COPY_BLOCKS=$cb ELECT_EC_COPY_VARIANT=$v run "lowcopy_b${cb}_v${v}_T${T:-8}_$i" 300 \
+                python bench.py --config hostpath --threads ${T:-8} --host-seconds 3 || exit $?
+        done; done; done ;;
     rs12)  # configs[4] with each launch's stream-mix probe
         for i in ${RS12_RUNS:-1 2}; do run "cfg_rs12_$i" 400 python bench.py --config rs12 || exit $?; done ;;
     padfill)  # padded encode vs content fill: where the time goes
