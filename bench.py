@@ -1035,7 +1035,6 @@ def config_hostpath(args, world, rank, dev):
         bufs.append((d, p))
     if pinned and not all(_lib.host_pinned(x.ctypes.data, L) for d, p in bufs for x in d + p):
         raise RuntimeError("--host-alloc pinned: elect_ec_host_alloc returned memory that is not page-locked")
-    calls = max(4, args.steps // 2) * max(1, 4404020 // L // 8) * ndev
     fused = args.host_op == "encode_ex"
     op = args.host_op
     # decode: each caller rebuilds its unit 0 into a unit of its own; update: a new version of
@@ -1054,52 +1053,63 @@ def config_hostpath(args, world, rank, dev):
 
     errors = []
     update_counts = [0] * T
+    # (start, end) of every call per caller; the rate counts the calls that END inside the
+    # timed window [t1, t2] of a free-running set of callers (each loops until told to stop:
+    # steady state, no join of all callers every few calls as before round 6, whose ramp-down
+    # and thread starts the rate used to include)
+    spans = [[] for _ in range(T)]
+    clock = time.perf_counter
+    go, stop = threading.Event(), threading.Event()
 
-    def worker(t, n):
+    def worker(t):
         try:
             if not args.host_devices:
                 torch.cuda.set_device(dev)
             d, p = bufs[t]
             da, pa = [x.ctypes.data for x in d], [x.ctypes.data for x in p]
-            if op == "decode":
-                surv, out = [pa[0]] + da[1:], [extra[t].ctypes.data]
-                for _ in range(n):
-                    coder.decode_host(surv, [4, 1, 2, 3], [0], out, L)
-                return
-            if op == "update":
-                ver = [da[1], extra[t].ctypes.data]  # the current and the next version of unit 1
-                for i in range(n):
+            rec = spans[t].append
+            go.wait()
+            i = 0
+            while not stop.is_set():
+                t0 = clock()
+                if op == "decode":
+                    coder.decode_host([pa[0]] + da[1:], [4, 1, 2, 3], [0], [extra[t].ctypes.data], L)
+                elif op == "update":
+                    ver = [da[1], extra[t].ctypes.data]  # the current and the next version of unit 1
                     coder.encode_update_host([ver[i % 2], ver[(i + 1) % 2]] + pa, 1, pa, L)
-                update_counts[t] += n
-                return
-            for _ in range(n):
-                if fused:
+                    update_counts[t] += 1
+                elif fused:
                     coder.encode_ex_host(da, pa, L, data_lengths=content, hashed=True)
                 else:
                     coder.encode_host(da, pa, L)
+                rec((t0, clock()))
+                i += 1
         except Exception as e:  # a failed call fails the run (a thread's exception would vanish)
             errors.append(f"caller {t}: {e!r}")
 
-    def run(n):
-        th = [threading.Thread(target=worker, args=(t, n)) for t in range(T)]
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
-        if errors:
-            raise RuntimeError(f"{len(errors)} caller(s) failed: {errors[0]}")
-
     import resource
-    run(1)  # warm: every caller's device, arenas and dispatchers
-    done, dt, cpu = 0, 0.0, 0.0
-    while done == 0 or dt < args.host_seconds:
-        r0 = resource.getrusage(resource.RUSAGE_SELF)
-        t0 = time.perf_counter()
-        run(calls)
-        dt += time.perf_counter() - t0
-        r1 = resource.getrusage(resource.RUSAGE_SELF)
-        cpu += (r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)
-        done += calls
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    window = args.host_seconds if args.host_seconds > 0 else 1.0
+    go.set()
+    time.sleep(max(0.3, min(1.0, window / 4)))  # warm: every caller's device, arenas, dispatchers, locks
+    r0, t1 = resource.getrusage(resource.RUSAGE_SELF), clock()
+    time.sleep(window)
+    r1, t2 = resource.getrusage(resource.RUSAGE_SELF), clock()
+    stop.set()
+    for x in th:
+        x.join()
+    if errors:
+        raise RuntimeError(f"{len(errors)} caller(s) failed: {errors[0]}")
+    dt = t2 - t1
+    cpu = (r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)
+    timed = [e - b for sp in spans for (b, e) in sp if t1 <= e <= t2]
+    if not timed:
+        raise RuntimeError(f"no call completed inside the {window:.1f} s window")
+    done_calls = len(timed)
+    done = max(1, round(done_calls / T))  # calls per caller (reported as steps)
+    calls_s = np.sort(np.asarray(timed))
     d, p = bufs[0]  # self-check through the product: rebuild d0 from [p0, d1, d2, d3]
     rebuilt = np.empty(L, np.uint8)
     coder.decode_host([p[0].ctypes.data] + [x.ctypes.data for x in d[1:]], [4, 1, 2, 3], [0],
@@ -1128,8 +1138,11 @@ def config_hostpath(args, world, rank, dev):
     op_name = {"encode_ex": "fused encode step (zero fill + encode + parity hashCode, elect_ec_encode_ex)",
                "decode": "single-erasure decode", "update": "parity update (encodeUpdate, in place)"}.get(op, "encode")
     # data = the bytes each call reads: k units (encode, decode), old + new + m parity (update)
-    data_gib = T * done * (2 + m if op == "update" else k) * L / GIB
+    data_gib = done_calls * (2 + m if op == "update" else k) * L / GIB
     stats = _lib.host_path_stats()
+    call_latency = {"p50": round(float(np.percentile(calls_s, 50)) * 1e3, 4),
+                    "p99": round(float(np.percentile(calls_s, 99)) * 1e3, 4),
+                    "mean": round(float(calls_s.mean()) * 1e3, 4), "calls": int(calls_s.size)}
     core_ms = cpu * 1e3 / data_gib
     quota = host_cpu_info()["quota_cores"] or len(os.sched_getaffinity(0))
     return {"metric": f"GiB/s host-memory RS(6,4) {op_name} through the C ABI (JNI calling convention)",
@@ -1142,9 +1155,12 @@ def config_hostpath(args, world, rank, dev):
             # the rate this path could reach if the process's CPU quota were its only limit
             "cpu_bound_ceiling_GiB/s": round(quota * 1e3 / core_ms, 1) if core_ms > 0 else None,
             "cpu_quota_cores": quota,
-            "steps": done, "warmup": 1, "ms_per_step": round(dt / done * 1e3, 3), "higher_is_better": True,
+            # wall time of one synchronous call, as its caller sees it (every timed call of every caller)
+            "call_latency_ms": call_latency,
+            "steps": done, "calls_timed": done_calls, "window_s": round(dt, 3), "warmup": 1,
+            "ms_per_step": round(dt / done * 1e3, 3), "higher_is_better": True,
             "scaling": "none", "vs_baseline": None, "dtype": "u8", "data": "synthetic", "verified": ok,
-            "config": {"workload": f"{T} threads x {done} synchronous elect_ec_{args.host_op} calls, one stripe "
+            "config": {"workload": f"{T} threads x ~{done} synchronous elect_ec_{args.host_op} calls, one stripe "
                                    f"of {k} x {L} B each, "
                                    f"{'elect_ec_host_alloc (page-locked)' if pinned else 'pageable'} host buffers, "
                                    f"over {ndev} device(s)",

@@ -145,11 +145,16 @@ SIGNATURES = [
 # "no ROCm-capable device is detected" in a test module that imported this
 # module before torch.  Importing torch first (where it is installed) makes
 # the library bind to torch's already-loaded runtime, as every torch-first
-# process already did.  (A JVM loads only the library's own runtime.)
-try:
-    import torch  # noqa: F401
-except ImportError:
-    pass
+# process already did.  (A JVM loads only the library's own runtime; the GPU
+# suite covers that path too: tools/hostpath_cbench, a C++ caller with no torch,
+# runs from tests/test_gpu_cbench.py.)  ELECT_EC_NO_TORCH=1 skips the import.
+# Any failure of a broken torch install is ignored here: the
+# library then loads /opt/rocm's runtime, as in a JVM.
+if os.environ.get("ELECT_EC_NO_TORCH") != "1":
+    try:
+        import torch  # noqa: F401
+    except Exception:  # noqa: BLE001
+        pass
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"{LIB_PATH} is missing: build the MI355X engine first "
@@ -237,12 +242,16 @@ def set_batching(enable: bool, window_us: int = 0, arena_bytes: int = 256 << 20)
 
 def host_path_stats() -> dict:
     """The host-memory path's counters (elect_ec_host_path_stats)."""
-    out = (ctypes.c_uint64 * 11)()
-    lib.elect_ec_host_path_stats(out, 11)
+    out = (ctypes.c_uint64 * 19)()
+    lib.elect_ec_host_path_stats(out, 19)
+    phases = ("lock", "fill", "queue", "issue", "device", "wake", "unlock")
     return {"zero_copy": out[0], "zero_copy_fallback": out[1], "batched": out[2], "per_thread": out[3],
             "direct": out[4], "registered": out[5], "register_fallback": out[6], "unregister_failures": out[7],
             "register_cpu_ms": round(out[8] * 1e-6, 1), "unregister_cpu_ms": round(out[9] * 1e-6, 1),
-            "dispatch_issue_cpu_ms": round(out[10] * 1e-6, 1)}
+            "dispatch_issue_cpu_ms": round(out[10] * 1e-6, 1),
+            # wall ms summed over calls (issue, device: over batches), and the batch count
+            "phase_ms": {name: round(out[11 + i] * 1e-6, 1) for i, name in enumerate(phases)},
+            "batches": out[18]}
 
 
 def host_alloc(nbytes: int) -> int:

@@ -38,7 +38,7 @@ using kern::ApplyParams;
 // also on hipEventBlockingSync events, and the runtime thread that runs
 // hipLaunchHostFunc callbacks; tools/tune/spin_probe.cpp, profiles/r05/
 // spin_probe.txt).  So the batcher's completions come from a poller thread per
-// device that queries events and sleeps in between (Batcher::wait_mode: 35 -> 17
+// device that queries events and sleeps in between (Batcher::poller: 35 -> 17
 // core-ms per GiB at 64 callers on pageable units, 28 -> 9 on pool units, the
 // same GiB/s; profiles/r05/completion_poll_ab.txt), and the per-thread engine
 // waits with wait_sleeping.  (Round 4's completion thread sleeping on
@@ -84,7 +84,8 @@ void stream_copy(uint8_t* dst, const uint8_t* src, size_t n)
 // Page-locked buffers for the callers' own units (elect_ec_host_alloc).  ELECT
 // allocates a direct ByteBuffer per unit and stripe and copies the SSTable into
 // it (ECMessageVerbHandler.java:298-314); when those buffers come from here,
-// the batcher moves a call's units by DMA straight between them and the device
+// the batcher's gather / scatter kernels move a call's units straight between
+// them and the device
 // (Batcher, direct batches): no staging copies, which are most of the CPU the
 // pageable path costs (1.5 bytes copied per data byte).
 // Pooled by size class (64 KiB steps): ELECT frees its buffers after every
@@ -162,8 +163,7 @@ public:
     // 46.9-47.7 from any hipHostMalloc kind (profiles/r05/pool_alloc_ab.txt).
     // The library reaches pool units only through kernels at their device
     // address (direct batches, zero-copy) or by CPU copies (the per-thread
-    // engine); round 4's per-piece hipMemcpyAsync A/B (ELECT_EC_DIRECT_MOVE=dma)
-    // wants "hip" blocks, which the HIP runtime knows as page-locked.
+    // engine).
     enum Kind { kHip, kNonCoherent, kCoherent, kHsaLock };
     static Kind kind()
     {
@@ -333,6 +333,35 @@ std::atomic<uint64_t> g_unregister_failures{0};
 // CPU time (ns, calling threads) spent registering, unregistering, and in the
 // dispatchers' issue() (host_path_stats entries 8-10, for the A/B of this path).
 std::atomic<uint64_t> g_register_cpu_ns{0}, g_unregister_cpu_ns{0}, g_issue_cpu_ns{0};
+// Where a batched call's wall time goes (host_path_stats entries 11-17, ns summed over
+// calls; 14 and 15 over batches, counted in entry 18): 0 entry -> units locked, 1 ->
+// arena edges copied and the call counted filled, 2 -> its batch's issue starts, 3 the
+// issue (dispatcher), 4 issue end -> the poller sees the batch done (device time and
+// polling delay), 5 -> the caller awake, 6 -> the call returns (edges out, unlocks).
+std::atomic<uint64_t> g_phase_ns[7];
+std::atomic<uint64_t> g_batches{0};
+thread_local int64_t t_phase_mark = 0;  // the calling thread's last phase boundary
+
+int64_t now_ns()
+{
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// ELECT_EC_PHASE_DEBUG=<us>: report calls whose fill phase took longer (diagnostics)
+int64_t phase_debug()
+{
+    static const int64_t ns = [] {
+        const char* e = std::getenv("ELECT_EC_PHASE_DEBUG");
+        return e ? static_cast<int64_t>(std::atoi(e)) * 1000 : int64_t{0};
+    }();
+    return ns;
+}
+
+void add_phase(int i, int64_t from, int64_t to)
+{
+    if (from && to > from) g_phase_ns[i].fetch_add(static_cast<uint64_t>(to - from), std::memory_order_relaxed);
+}
 
 uint64_t thread_cpu_ns()
 {
@@ -571,67 +600,6 @@ struct DirectPlan {
     int nheld = 0;
 };
 
-// Direct batches move their units by gather / scatter kernels (the default) or,
-// with ELECT_EC_DIRECT_MOVE=dma, by a hipMemcpyAsync per piece (round 4's way;
-// page-locked pool units only: no per-call locking then).
-bool direct_by_kernel()
-{
-    static const bool k = [] {
-        const char* e = std::getenv("ELECT_EC_DIRECT_MOVE");
-        return !(e && std::string(e) == "dma");
-    }();
-    return k;
-}
-
-// ELECT_EC_DIRECT_MOVE=sdma: the direct units' H2D by the GPU's DMA engines
-// (hsa_amd_memory_async_copy from the locked / pool memory) instead of the
-// gather kernel, whose host reads top out near 49 GB/s; the ends and the
-// scatter stay kernels.  (A/B.)
-bool direct_h2d_sdma()
-{
-    static const bool k = [] {
-        const char* e = std::getenv("ELECT_EC_DIRECT_MOVE");
-        return e && std::string(e) == "sdma";
-    }();
-    return k;
-}
-
-// Bytes per gather / scatter piece (ELECT_EC_PIECE_KB, 4..64, default 64): the
-// copy kernels' blocks take pieces round robin, so a launch ends with a tail of
-// at most one piece per block.
-size_t piece_bytes()
-{
-    static const size_t b = [] {
-        const char* e = std::getenv("ELECT_EC_PIECE_KB");
-        const int kb = e ? std::atoi(e) : 64;
-        return static_cast<size_t>(std::min(64, std::max(4, kb))) << 10;
-    }();
-    return b;
-}
-
-// A CPU agent (the source side of host-to-device HSA copies).
-bool hsa_cpu_agent(hsa_agent_t* out)
-{
-    static const std::pair<bool, hsa_agent_t> a = [] {
-        std::pair<bool, hsa_agent_t> r{false, {}};
-        if (hsa_init() != HSA_STATUS_SUCCESS) return r;
-        hsa_iterate_agents(
-            [](hsa_agent_t ag, void* arg) -> hsa_status_t {
-                hsa_device_type_t t{};
-                if (hsa_agent_get_info(ag, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
-                    auto* p = static_cast<std::pair<bool, hsa_agent_t>*>(arg);
-                    *p = {true, ag};
-                    return HSA_STATUS_INFO_BREAK;
-                }
-                return HSA_STATUS_SUCCESS;
-            },
-            &r);
-        return r;
-    }();
-    *out = a.second;
-    return a.first;
-}
-
 // Per-call page locking of batched callers' pageable units (ELECT_EC_REGISTER:
 // 0 off, 1 on, the default; units of at least kMinBytes): each unit's interior
 // pages are locked with hsa_amd_memory_lock (Registrar), the batch's
@@ -664,7 +632,7 @@ struct RegisterPath {
     // interiors share it).  False (nothing held): take the staged path.
     static bool plan(const HostOp& op, size_t len, int dev, DirectPlan& dp)
     {
-        if (mode() != 1 || len < kMinBytes || !direct_by_kernel()) return false;
+        if (mode() != 1 || len < kMinBytes) return false;
         RegisterSlots& slots = RegisterSlots::get();
         if (RegisterSlots::wait())
             slots.take();
@@ -831,7 +799,7 @@ void run_copies(const std::vector<CopyJob>& jobs, bool lone)
 }
 
 // Waits for ev without spinning a core: this HIP runtime's own waits spin for as
-// long as the work they wait for runs (Batcher::wait_mode); hipEventQuery with
+// long as the work they wait for runs (Batcher::poller); hipEventQuery with
 // sleeps from 2 up to 50 us costs ~2 % of a core instead.
 hipError_t wait_sleeping(hipEvent_t ev)
 {
@@ -1141,6 +1109,7 @@ class Batcher {
 public:
     static constexpr int kFallback = 1000;  // request does not fit (or no arena): run it directly
     static constexpr int kMaxSlabs = 4;  // arenas per device (ELECT_EC_BATCH_SLABS, default 3)
+    static constexpr int kMaxSteps = 8;  // pipeline steps of a direct batch (ELECT_EC_PIPELINE_STEPS)
     // Per-slot content lengths (padded ops) and parity hashes (hashed ops) of a
     // batch: entries per arena, which caps such a batch's stripes.
     static constexpr size_t kMetaEntries = size_t{1} << 16;
@@ -1159,9 +1128,10 @@ public:
 
     explicit Batcher(int dev) : dev_(dev) {}
 
-    // dp (a direct call, dp->direct): its units move by DMA between the caller's
-    // page-locked memory (pool buffers, or units registered for the call) and
-    // the device, with no staging copies, in batches of direct calls only;
+    // dp (a direct call, dp->direct): its units move by the batch's gather /
+    // scatter kernels between the caller's page-locked memory (pool buffers, or
+    // units locked for the call) and the device, with no staging copies, in
+    // batches of direct calls only (pipelined in steps, issue_direct);
     // bytes outside a unit's [lo, hi) (a registered unit's partial end pages)
     // go through the arena, copied by this caller.  nullptr: staged.
     int submit(const HostOp& op, size_t len, const DirectPlan* dp)
@@ -1173,7 +1143,7 @@ public:
             ~InFlight() { n.fetch_sub(1); }
         } in_flight(callers_);
         // untiled: one unit per column at a 256-byte pitch; tiled: T tiles of 64 KiB
-        // (direct batches are untiled: one DMA per unit)
+        // (direct batches are untiled: the gather pieces land at unit offsets)
         const size_t tile = direct ? 0 : batch_config().tile.load();
         // (tiled launches ride on the padded vector kernels: a wider product, the
         // update of an m >= 9 code, stays untiled rather than fail its whole batch)
@@ -1185,7 +1155,9 @@ public:
         std::vector<CopyJob>& jobs = t_jobs;
         jobs.clear();
         jobs.reserve(static_cast<size_t>(std::max(op.cols, op.rows)) * (tiles + (len >> 20) + 1));
+        const int64_t t_sub0 = now_ns();
         std::unique_lock<std::mutex> lock(mu_);
+        const int64_t t_sub1 = now_ns();
         if (init_failed_) return kFallback;
         if (!started_) {  // arenas, streams and events once, before anything is in flight
             if (init(batch_config().arena_bytes.load()) != ELECT_EC_OK) {
@@ -1196,7 +1168,7 @@ public:
             }
             try {
                 std::thread(&Batcher::worker, this).detach();  // lives as long as the process
-                if (wait_mode() == kWaitPoll) std::thread(&Batcher::poller, this).detach();
+                std::thread(&Batcher::poller, this).detach();
             } catch (...) {  // no dispatcher: the per-thread engine serves every call
                 release();
                 init_failed_ = true;
@@ -1224,6 +1196,7 @@ public:
             cv_worker_.notify_one();  // the open batch was closed: let it leave
             cv_slot_.wait(lock);      // until an arena is free again
         }
+        const int64_t t_sub2 = now_ns();
         const int slot = slab->reserved++;
         slab->readers++;
         if (slab->reserved == slab->capacity) slab->full = true;
@@ -1236,7 +1209,7 @@ public:
         for (int j = 0; j < op.cols; ++j) {
             const size_t n = op.lens ? op.lens[j] : len;  // padded: only the content bytes
             if (op.lens) slab->pin_lens[static_cast<size_t>(slot) * op.cols + j] = static_cast<uint32_t>(n);
-            if (direct) {  // the dispatcher DMAs [lo, hi) from the caller's buffer, the rest from the arena
+            if (direct) {  // the gather reads [lo, hi) from the caller's buffer, the rest from the arena
                 const size_t i = static_cast<size_t>(slot) * kern::kMaxCols + j;
                 const size_t lo = std::min(dp->in_lo[j], n), hi = std::min(std::max(dp->in_hi[j], lo), n);
                 // the unit's base at its device address ([lo, hi) is what the gather reads there)
@@ -1263,13 +1236,22 @@ public:
         }
         if (!jobs.empty()) run_copies(jobs, !direct && callers_.load() <= lone_callers());  // fenced before the H2D
 
+        const int64_t t_filled = now_ns();
+        add_phase(1, t_phase_mark, t_filled);
+        if (phase_debug() && t_filled - t_phase_mark > phase_debug())
+            std::fprintf(stderr, "elect_ec slow fill: %.1f us (enter %.1f, mutex %.1f, slab %.1f, copies %.1f)\n",
+                         (t_filled - t_phase_mark) * 1e-3, (t_sub0 - t_phase_mark) * 1e-3, (t_sub1 - t_sub0) * 1e-3,
+                         (t_sub2 - t_sub1) * 1e-3, (t_filled - t_sub2) * 1e-3);
         lock.lock();
         if (++slab->filled == slab->reserved) cv_worker_.notify_one();
         slab->done.wait(lock, [&] { return slab->state == Slab::kDone; });
         const int status = slab->status;
+        t_phase_mark = now_ns();
+        add_phase(2, t_filled, slab->t_issue0);
+        add_phase(5, slab->t_finish, t_phase_mark);
         lock.unlock();
 
-        if (status == ELECT_EC_OK && direct) {  // the D2H wrote [lo, hi) of each output; the rest is in the arena
+        if (status == ELECT_EC_OK && direct) {  // the scatter wrote [lo, hi) of each output; the rest is in the arena
             const uint8_t* const out_base = slab->pin_out + slot * (op.rows * pitch);
             jobs.clear();
             for (int r = 0; r < op.rows; ++r) {
@@ -1312,7 +1294,7 @@ private:
     // dispatcher (the callers write them before taking mu_ to count themselves
     // filled).  issue() reads only this copy: the slab's arrays are rewritten for
     // its next batch once this one completes, and the only order between that and
-    // issue()'s reads would otherwise run through the HIP stream (ThreadSanitizer,
+    // issue()'s reads would otherwise run through the HIP streams (ThreadSanitizer,
     // profiles/r04/tsan_summary.txt).
     struct DirectSlots {
         std::vector<const uint8_t*> src;
@@ -1333,15 +1315,16 @@ private:
         uint64_t seq = 0;
         std::chrono::steady_clock::time_point opened;
         uint8_t *pin_in = nullptr, *pin_out = nullptr, *d_in = nullptr, *d_out = nullptr;
-        uint32_t *pin_lens = nullptr, *d_lens = nullptr;  // [slot][cols]
+        uint32_t *pin_lens = nullptr, *d_lens = nullptr;  // [slot][cols]; direct batches: [step][slot][cols]
         int32_t *pin_hash = nullptr, *d_hash = nullptr;    // [slot][rows]
-        // direct batches: the arenas' device addresses, and the gather + scatter
-        // piece table (page-locked, read by the copy kernels where it lies)
+        // direct batches: the arenas' and metadata's device addresses, and the
+        // gather + scatter piece table (page-locked, read by the copy kernels where it lies)
         uint8_t *pin_in_dev = nullptr, *pin_out_dev = nullptr;
+        uint8_t *pin_lens_dev = nullptr, *pin_hash_dev = nullptr;
         kern::CopyPiece* pieces = nullptr;
         const kern::CopyPiece* pieces_dev = nullptr;
         size_t max_pieces = 0;
-        uint32_t* d_scratch = nullptr;                       // hash partials of the batch's launch
+        uint32_t* d_scratch = nullptr;                       // hash partials of the batch's launches
         size_t scratch_words = 0;
         // direct batches: each slot's unit pointers, input byte counts and the
         // [lo, hi) moved straight from / to the caller's memory, [slot][kMaxCols / kMaxRows]
@@ -1350,12 +1333,15 @@ private:
         std::unique_ptr<uint8_t*[]> ddst;
         std::unique_ptr<size_t[]> ddst_lo, ddst_hi;
         std::condition_variable done;  // this batch's callers wait here for kDone
-        hipStream_t stream = nullptr;
+        // h2d_done: the batch's inputs have (nearly) all landed, the dispatch gate
+        // (on the gather stream, behind the gate step); done_ev: behind its last
+        // operation (on the scatter stream).  Both polled (Batcher::poller).
+        hipStream_t stream = nullptr;  // the slab's batches, in order
         hipEvent_t h2d_done = nullptr;
-        hipEvent_t done_ev = nullptr;  // recorded behind the batch's last operation (completion by polling)
-        hsa_signal_t sig{};  // counts a direct batch's outstanding HSA copies (ELECT_EC_DIRECT_MOVE=sdma)
-        bool h2d_landed = false;  // the batch in flight has its inputs on the device (under the owner's mu_)
-        bool issued = false;      // ... and all of its work is enqueued, events recorded (poll mode)
+        hipEvent_t done_ev = nullptr;
+        int64_t t_issue0 = 0, t_issue1 = 0, t_finish = 0;  // phase marks (now_ns, under the owner's mu_)
+        bool h2d_landed = false;  // the batch in flight has passed its gate (under the owner's mu_)
+        bool issued = false;      // ... and all of its work is enqueued, events recorded
 
         Shape shape() const
         {
@@ -1407,16 +1393,21 @@ private:
     {
         arena_ = arena;
         nslabs_ = batch_config().slabs.load();
+        // One stream per slab carries its batch: a batch's steps run in stream order
+        // (issue_direct), and batches overlap each other on their own streams (the next
+        // batch's gathers beside this one's last scatter) with no dependency between
+        // streams.  (A round-6 A/B chained three per-device streams -- gathers, coding,
+        // scatters -- for overlap inside a batch: waiting on events across streams
+        // (hipStreamWaitEvent) kept a runtime thread at 73 % of a core, 35-44 core-ms
+        // per GiB; device-side waits on memory (hipStreamWaitValue64) cost no host CPU
+        // but are blit kernels of 4-20 us per handoff on the queues, and the gathers
+        // ran at 46 against 53 GB/s beside concurrent scatters: no faster than one
+        // step.  tools/tune/spin_probe.cpp chain_*, profiles/r06/spin_chain.txt,
+        // profiles/r06/pipeline_chain_ab.txt.)
         for (Slab& s : active()) {
             s.owner = this;
             hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
-            // ELECT_EC_DISPATCH_BLOCKING=1: the dispatcher sleeps on the event instead of polling it (A/B)
-            static const bool blocking = [] {
-                const char* b = std::getenv("ELECT_EC_DISPATCH_BLOCKING");
-                return b && std::atoi(b) > 0;
-            }();
-            if (e == hipSuccess)
-                e = hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming | (blocking ? hipEventBlockingSync : 0));
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming);
             // device first: an arena too large for the device fails there, before any host pinning
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_in), arena);
@@ -1427,8 +1418,10 @@ private:
             if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_lens), meta, hipHostMallocDefault);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_lens), meta);
             if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.pin_hash), meta, hipHostMallocDefault);
-            // gather: <= one piece per 64 KiB of the arena plus 3 per unit; the scatter as many
-            s.max_pieces = 2 * (arena / piece_bytes() + 3 * kMaxDirectSlots * std::max(kern::kMaxCols, kern::kMaxRows));
+            // one step, the smallest pieces: one per 16 KiB of the arena plus 3 per unit, both
+            // ways, and the lens and hash pieces (plan_steps checks a pipelined batch's count)
+            s.max_pieces = 2 * (arena / kMinPiece + 3 * kMaxDirectSlots * std::max(kern::kMaxCols, kern::kMaxRows)) +
+                           2 * (meta / kMinPiece + 1);
             if (e == hipSuccess)
                 e = hipHostMalloc(reinterpret_cast<void**>(&s.pieces), s.max_pieces * sizeof(kern::CopyPiece),
                                   hipHostMallocDefault);
@@ -1439,8 +1432,10 @@ private:
             s.pin_in_dev = static_cast<uint8_t*>(dv);
             if (e == hipSuccess) e = hipHostGetDevicePointer(&dv, s.pin_out, 0);
             s.pin_out_dev = static_cast<uint8_t*>(dv);
-            if (e == hipSuccess && direct_h2d_sdma() && hsa_signal_create(0, 0, nullptr, &s.sig) != HSA_STATUS_SUCCESS)
-                s.sig.handle = 0;
+            if (e == hipSuccess) e = hipHostGetDevicePointer(&dv, s.pin_lens, 0);
+            s.pin_lens_dev = static_cast<uint8_t*>(dv);
+            if (e == hipSuccess) e = hipHostGetDevicePointer(&dv, s.pin_hash, 0);
+            s.pin_hash_dev = static_cast<uint8_t*>(dv);
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_hash), meta);
             s.scratch_words = kern::hash_scratch_need(arena / 16);  // a batch has at most arena/16 segments
             if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_scratch), s.scratch_words * sizeof(uint32_t));
@@ -1460,6 +1455,8 @@ private:
             for (auto* v : {&slots_.dst_lo, &slots_.dst_hi}) v->reserve(kMaxDirectSlots * kern::kMaxRows);
             slots_.src.reserve(kMaxDirectSlots * kern::kMaxCols);
             slots_.dst.reserve(kMaxDirectSlots * kern::kMaxRows);
+            gbuf_.reserve(slabs_[0].max_pieces);
+            sbuf_.reserve(slabs_[0].max_pieces);
         } catch (const std::bad_alloc&) {
             return ELECT_EC_ENOMEM;
         }
@@ -1471,8 +1468,11 @@ private:
     {
         for (Slab& s : active()) {
             if (s.stream) (void)hipStreamDestroy(s.stream);
-            if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
-            if (s.done_ev) (void)hipEventDestroy(s.done_ev);
+            s.stream = nullptr;
+            for (hipEvent_t* ev : {&s.h2d_done, &s.done_ev}) {
+                if (*ev) (void)hipEventDestroy(*ev);
+                *ev = nullptr;
+            }
             for (uint8_t* h : {s.pin_in, s.pin_out})
                 if (h) (void)hipHostFree(h);
             for (void* h : {static_cast<void*>(s.pin_lens), static_cast<void*>(s.pin_hash), static_cast<void*>(s.pieces)})
@@ -1480,25 +1480,31 @@ private:
             for (void* d : {static_cast<void*>(s.d_in), static_cast<void*>(s.d_out), static_cast<void*>(s.d_lens),
                             static_cast<void*>(s.d_hash), static_cast<void*>(s.d_scratch)})
                 if (d) (void)hipFree(d);
-            s.stream = nullptr;
-            s.h2d_done = nullptr;
-            s.done_ev = nullptr;
             s.pin_in = s.pin_out = s.d_in = s.d_out = nullptr;
             s.pin_lens = s.d_lens = nullptr;
             s.pin_hash = s.d_hash = nullptr;
             s.pieces = nullptr;
             s.pieces_dev = nullptr;
-            s.pin_in_dev = s.pin_out_dev = nullptr;
+            s.pin_in_dev = s.pin_out_dev = s.pin_lens_dev = s.pin_hash_dev = nullptr;
             s.d_scratch = nullptr;
         }
         arena_ = 0;
     }
 
-    // Self-clocking dispatch: a batch leaves as soon as the previous batch's
-    // inputs have landed on the device (or at once on an idle device), so the
-    // next H2D overlaps the previous kernel and D2H; callers keep filling the
-    // other arena meanwhile.  An optional window (ELECT_EC_BATCH_WINDOW_US) caps
-    // how long an idle device waits for more callers; 0 = never wait.
+    // Waits for everything queued on a slab's stream (error paths only: it spins a
+    // core, see wait_sleeping).
+    static void drain(Slab& s)
+    {
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        (void)hipGetLastError();
+    }
+
+    // Self-clocking dispatch: a batch leaves as soon as the previous batch has
+    // passed its gate (its inputs have landed: a pipelined batch's last gather
+    // stage is done, its last coding launch and scatter may still run beside the
+    // new batch's first gathers), or at once on an idle device; callers keep
+    // filling the other arenas meanwhile.  An optional window (ELECT_EC_BATCH_WINDOW_US) caps how
+    // long an idle device waits for more callers; 0 = never wait.
     void worker()
     {
         pthread_setname_np(pthread_self(), ("ec-dispatch" + std::to_string(dev_)).c_str());
@@ -1513,15 +1519,8 @@ private:
                     if (x.state == Slab::kOpen && (!s || x.seq < s->seq)) s = &x;
                 return s != nullptr;
             });
-            if (prev && prev->state == Slab::kInFlight) {  // wait for its H2D only
-                if (wait_mode() != kWaitEvent) {  // asleep until the poller / on_h2d sees prev's inputs land
-                    cv_worker_.wait(lock, [&] { return prev->h2d_landed || prev->state != Slab::kInFlight; });
-                } else {
-                    hipEvent_t ev = prev->h2d_done;
-                    lock.unlock();
-                    (void)hipEventSynchronize(ev);
-                    lock.lock();
-                }
+            if (prev && prev->state == Slab::kInFlight) {  // asleep until the poller sees prev pass its gate
+                cv_worker_.wait(lock, [&] { return prev->h2d_landed || prev->state != Slab::kInFlight; });
             } else {
                 const unsigned w = batch_config().window_us.load();
                 if (w) cv_worker_.wait_until(lock, s->opened + std::chrono::microseconds(w), [&] { return s->full; });
@@ -1542,15 +1541,21 @@ private:
                 slots_.dst_lo.assign(s->ddst_lo.get(), s->ddst_lo.get() + no);
                 slots_.dst_hi.assign(s->ddst_hi.get(), s->ddst_hi.get() + no);
             }
+            s->t_issue0 = now_ns();
+            s->t_issue1 = 0;
             lock.unlock();
             const uint64_t t0 = thread_cpu_ns();
-            const hipError_t e = issue(*s, shape, n, slots_);
+            const hipError_t e = shape.direct ? issue_direct(*s, shape, n, slots_) : issue_staged(*s, shape, n);
             g_issue_cpu_ns.fetch_add(thread_cpu_ns() - t0);
-            if (e != hipSuccess) (void)hipStreamSynchronize(s->stream);  // no completion was queued
+            if (e != hipSuccess) drain(*s);  // no completion was queued: nothing of it may still run
+            const int64_t t_issued = now_ns();
+            add_phase(3, s->t_issue0, t_issued);
+            g_batches.fetch_add(1, std::memory_order_relaxed);
             lock.lock();
+            s->t_issue1 = t_issued;
             if (e != hipSuccess) {
                 finish(s, map_hip(e));
-            } else if (wait_mode() == kWaitPoll) {
+            } else {
                 s->issued = true;
                 cv_poll_.notify_one();
             }
@@ -1558,107 +1563,248 @@ private:
         }
     }
 
-    // s's buffers, stream and event never change after init(); its shape is
-    // read from the copy taken under mu_.
-    static hipError_t issue(Slab& s, const Shape& sh, int n, const DirectSlots& d)
+    // ---- steps of a direct batch (round 6) ------------------------------------
+    // A direct batch runs in S steps over windows of its units' bytes, all on the
+    // slab's one stream, as a software pipeline of copy stages and coding
+    // launches:
+    //   copy(G0)  code(0)  copy(G1 + S0)  code(1)  ...  code(S-1)  copy(S[S-1])
+    // Gk gathers window k of every unit, Sk scatters window k of every output;
+    // one copy stage moves window k+1 in and window k-1 out at once (gather and
+    // scatter pieces interleaved in one launch of the copy kernel), so both PCIe
+    // directions are busy inside one call and a lone caller's call is no longer
+    // gather -> code -> scatter in series (round 5: 330 + 18 + 163 us per 4.4 MB
+    // RS(6,4) stripe, profiles/r06/hostprof_t1_before.txt).  Stream order is
+    // the only synchronisation: code(k) follows the stage that gathered window k,
+    // the stage after it scatters what code(k) wrote.  S grows with the batch's
+    // input bytes (one step per ELECT_EC_STEP_KB, default 4 MiB, at most
+    // ELECT_EC_PIPELINE_STEPS, default 8; windows of at least 256 KiB,
+    // multiples of 64 KiB).  Each coding launch takes its window: plain where the
+    // window is whole 16-byte segments, padded with the window's length for the
+    // last window's partial segment (no separate byte-granular tail launch),
+    // padded ops with per-step content lengths ([step][slot][cols] in the slab's
+    // lens arrays, moved by the first stage), hashed ops adding each window's
+    // terms (31^(window offset + i)) into entries seeded 31^len.
+    struct Steps {
+        int n = 1;          // steps
+        size_t window = 0;  // unit bytes per step (the last takes the rest)
+        size_t piece = 0;   // gather / scatter piece bytes
+    };
+    static constexpr size_t kMinWindow = size_t{256} << 10;
+    static constexpr size_t kMinPiece = size_t{16} << 10;
+
+    static int max_steps()
     {
-        const size_t in_stride = sh.tiles * sh.cols * sh.pitch;  // per slot
-        const size_t out_stride = sh.tiles * sh.rows * sh.pitch;
-        hipError_t e = hipSuccess;
-        // Direct batches: each unit's [lo, hi) straight from its caller's page-locked
-        // memory, the rest (a locked unit's partial end pages) from the arena.
-        // By kernel (the default): one gather launch reads every piece over PCIe
-        // into the device arena, one scatter launch writes the outputs back; the
-        // piece table is written here and read by the kernels where it lies.
-        // By DMA (ELECT_EC_DIRECT_MOVE=dma, round 4's way, pool units only): a
-        // hipMemcpyAsync per piece, all on the slab's one stream (spreading them
-        // over two streams lost 6-8 GiB/s at 16 and 64 callers,
-        // profiles/r04/direct_streams_ab.txt); pieces contiguous on both sides
-        // with the one before share its DMA.
-        const bool by_kernel = direct_by_kernel();
-        size_t gather_n = 0, scatter_n = 0;
-        if (sh.direct && by_kernel) {
-            size_t np = 0;
-            bool overflow = false;
-            // sdma: the units' [lo, hi) by hsa_amd_memory_async_copy, all counted down on s.sig
-            hsa_agent_t gpu{}, cpu{};
-            const bool sdma = direct_h2d_sdma() && s.sig.handle && hsa_agent_of(s.owner->dev_, &gpu) && hsa_cpu_agent(&cpu);
-            int64_t ncopies = 0;
-            if (sdma) {
+        static const int s = [] {
+            const char* e = std::getenv("ELECT_EC_PIPELINE_STEPS");
+            return e ? std::min(kMaxSteps, std::max(1, std::atoi(e))) : kMaxSteps;
+        }();
+        return s;
+    }
+    static size_t step_target()
+    {
+        static const size_t b = [] {
+            const char* e = std::getenv("ELECT_EC_STEP_KB");
+            return (e && std::atoi(e) > 0 ? static_cast<size_t>(std::atoi(e)) : size_t{4096}) << 10;
+        }();
+        return b;
+    }
+    // ELECT_EC_PIECE_KB (16..64): a fixed piece size; default: 64 KiB pieces for
+    // stages of at least 16 MiB (two rounds of 64 KiB pieces over the copy
+    // kernels' 128 blocks; round 5's 64-caller batches measured best at 64 KiB,
+    // hostpath_low_concurrency.txt), 16 KiB below, so a lone caller's few-MiB
+    // stage still spreads over every copy block with a short last round.
+    static size_t piece_for(size_t stage_bytes)
+    {
+        static const size_t fixed = [] {
+            const char* e = std::getenv("ELECT_EC_PIECE_KB");
+            return e ? static_cast<size_t>(std::min(64, std::max(16, std::atoi(e)))) << 10 : size_t{0};
+        }();
+        if (fixed) return fixed;
+        return stage_bytes >= (size_t{16} << 20) ? kern::kMaxPieceBytes : kMinPiece;
+    }
+
+    // ELECT_EC_PIPELINE_ALONE (default 1): pipeline a batch only when its callers
+    // are all the callers in flight on the device.  With more callers, batches
+    // already overlap one another (the next batch's gathers beside this one's
+    // coding and scatter), and the steps' extra launches cost more than they
+    // give: 2 / 4 / 8 callers 33.6-35.4 / 38.2-39.0 / 41.8-42.7 GiB/s pipelined
+    // against 39.4-40.6 / 42.2-43.9 / 44.2-45.5 in one step, one caller 29.5-30.3
+    // against 27.1-29.4 on the same box (35.0 against 28.4-29.2 on another),
+    // profiles/r06/pipeline_ab.txt.
+    static bool pipeline_alone_only()
+    {
+        static const bool a = [] {
+            const char* e = std::getenv("ELECT_EC_PIPELINE_ALONE");
+            return !(e && std::atoi(e) == 0);
+        }();
+        return a;
+    }
+
+    Steps plan_steps(const Shape& sh, int n, const DirectSlots& d) const
+    {
+        size_t in_bytes = 0;
+        for (int q = 0; q < n; ++q)
+            for (int j = 0; j < sh.cols; ++j) in_bytes += d.src_n[static_cast<size_t>(q) * kern::kMaxCols + j];
+        int s = static_cast<int>(std::min<size_t>(max_steps(), std::max<size_t>(1, (in_bytes + step_target() - 1) / step_target())));
+        if (pipeline_alone_only() && callers_.load() > n) s = 1;  // other callers wait: batches overlap instead
+        s = static_cast<int>(std::min<size_t>(s, std::max<size_t>(1, sh.len / kMinWindow)));
+        if (sh.padded) s = static_cast<int>(std::min<size_t>(s, std::max<size_t>(1, kMetaEntries / (static_cast<size_t>(n) * sh.cols))));
+        Steps st;
+        constexpr size_t kAlign = size_t{1} << 16;
+        st.window = s > 1 ? ((sh.len + s - 1) / s + kAlign - 1) / kAlign * kAlign : sh.len;
+        st.n = static_cast<int>((sh.len + st.window - 1) / st.window);
+        st.piece = piece_for((in_bytes + static_cast<size_t>(n) * sh.rows * sh.len) / st.n);
+        return st;
+    }
+
+    // Writes the direct batch's piece table for `st`: stage k (0..S) holds the
+    // gather pieces of window k (k < S) and the scatter pieces of window k-1
+    // (k >= 1), interleaved in proportion so that both directions run through
+    // the whole launch; stage k is [begin[k], begin[k + 1]).  False when it does
+    // not fit the slab's table.
+    static bool write_pieces(Slab& s, const Shape& sh, int n, const DirectSlots& d, const Steps& st, size_t* begin,
+                             std::vector<kern::CopyPiece>& gbuf, std::vector<kern::CopyPiece>& sbuf)
+    {
+        const size_t in_stride = sh.cols * sh.pitch, out_stride = sh.rows * sh.pitch;
+        size_t np = 0;
+        bool room = true;  // (the lists never grow past what init() reserved: no allocation here)
+        auto put = [&](std::vector<kern::CopyPiece>& v, const uint8_t* from, uint8_t* to, size_t bytes) {
+            for (size_t o = 0; o < bytes && room; o += st.piece) {
+                if (v.size() == v.capacity()) room = false;
+                else v.push_back(kern::CopyPiece{from + o, to + o, static_cast<uint32_t>(std::min(st.piece, bytes - o)), 0});
+            }
+        };
+        // [a, b) of a unit clipped to the window [w0, w1): from + x -> to + x
+        auto seg = [&](std::vector<kern::CopyPiece>& v, size_t a, size_t b, size_t w0, size_t w1, const uint8_t* from,
+                       uint8_t* to) {
+            const size_t x = std::max(a, w0), y = std::min(b, w1);
+            if (x < y) put(v, from + x, to + x, y - x);
+        };
+        for (int k = 0; k <= st.n; ++k) {
+            gbuf.clear();
+            sbuf.clear();
+            if (k < st.n) {  // gather window k
+                const size_t w0 = k * st.window, w1 = std::min(sh.len, w0 + st.window);
+                if (k == 0 && sh.padded)  // the per-step content lengths ride in the first stage
+                    put(gbuf, s.pin_lens_dev, reinterpret_cast<uint8_t*>(s.d_lens),
+                        static_cast<size_t>(st.n) * n * sh.cols * sizeof(uint32_t));
                 for (int q = 0; q < n; ++q)
                     for (int j = 0; j < sh.cols; ++j) {
                         const size_t i = static_cast<size_t>(q) * kern::kMaxCols + j;
-                        ncopies += d.src_hi[i] > d.src_lo[i];
+                        const size_t nb = d.src_n[i], lo = d.src_lo[i], hi = d.src_hi[i];
+                        uint8_t* const dev = s.d_in + q * in_stride + j * sh.pitch;
+                        const uint8_t* const pin = s.pin_in_dev + q * in_stride + j * sh.pitch;
+                        seg(gbuf, 0, lo, w0, w1, pin, dev);
+                        seg(gbuf, lo, hi, w0, w1, d.src[i], dev);
+                        seg(gbuf, hi, nb, w0, w1, pin, dev);
                     }
-                hsa_signal_store_screlease(s.sig, ncopies);
             }
-            bool copy_failed = false;
-            auto piece = [&](const uint8_t* from, uint8_t* to, size_t bytes) {
-                for (size_t o = 0; o < bytes; o += piece_bytes()) {
-                    if (np == s.max_pieces) {
-                        overflow = true;
-                        return;
+            if (k >= 1) {  // scatter window k-1
+                const size_t w0 = (k - 1) * st.window, w1 = std::min(sh.len, w0 + st.window);
+                for (int q = 0; q < n; ++q)
+                    for (int r = 0; r < sh.rows; ++r) {
+                        const size_t i = static_cast<size_t>(q) * kern::kMaxRows + r;
+                        const size_t lo = d.dst_lo[i], hi = d.dst_hi[i];
+                        const uint8_t* const dev = s.d_out + q * out_stride + r * sh.pitch;
+                        uint8_t* const pin = s.pin_out_dev + q * out_stride + r * sh.pitch;
+                        seg(sbuf, 0, lo, w0, w1, dev, pin);
+                        seg(sbuf, lo, hi, w0, w1, dev, d.dst[i]);
+                        seg(sbuf, hi, sh.len, w0, w1, dev, pin);
                     }
-                    s.pieces[np++] = kern::CopyPiece{from + o, to + o,
-                                                     static_cast<uint32_t>(std::min<size_t>(piece_bytes(), bytes - o)), 0};
-                }
-            };
-            for (int q = 0; q < n; ++q)
-                for (int j = 0; j < sh.cols; ++j) {
-                    const size_t i = static_cast<size_t>(q) * kern::kMaxCols + j;
-                    const size_t nb = d.src_n[i], lo = d.src_lo[i], hi = d.src_hi[i];
-                    uint8_t* const dev = s.d_in + q * in_stride + j * sh.pitch;
-                    const uint8_t* const pin = s.pin_in_dev + q * in_stride + j * sh.pitch;
-                    piece(pin, dev, lo);
-                    if (!sdma)
-                        piece(d.src[i] + lo, dev + lo, hi - lo);
-                    else if (hi > lo && hsa_amd_memory_async_copy(dev + lo, gpu, d.src[i] + lo, cpu, hi - lo, 0, nullptr,
-                                                                 s.sig) != HSA_STATUS_SUCCESS) {
-                        copy_failed = true;
-                        hsa_signal_subtract_screlease(s.sig, 1);  // the copy that was never queued
-                    }
-                    piece(pin + hi, dev + hi, nb - hi);
-                }
-            gather_n = np;
-            for (int q = 0; q < n; ++q)
-                for (int r = 0; r < sh.rows; ++r) {
-                    const size_t i = static_cast<size_t>(q) * kern::kMaxRows + r;
-                    const size_t lo = d.dst_lo[i], hi = d.dst_hi[i];
-                    const uint8_t* const dev = s.d_out + q * out_stride + r * sh.pitch;
-                    uint8_t* const pin = s.pin_out_dev + q * out_stride + r * sh.pitch;
-                    piece(dev, pin, lo);
-                    piece(dev + lo, d.dst[i] + lo, hi - lo);
-                    piece(dev + hi, pin + hi, sh.len - hi);
-                }
-            scatter_n = np - gather_n;
-            e = overflow ? hipErrorInvalidValue
-                         : kern::launch_copy_pieces(s.pieces_dev, static_cast<uint32_t>(gather_n), s.stream);
-            if (sdma && ncopies) {  // the coding launch below reads them: wait here, off every caller's thread
-                const hsa_signal_value_t v = hsa_signal_wait_scacquire(s.sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
-                                                                       HSA_WAIT_STATE_BLOCKED);
-                if ((v < 0 || copy_failed) && e == hipSuccess) e = hipErrorLaunchFailure;
+                if (k == st.n && sh.hashed)  // the parity hashes ride in the last stage
+                    put(sbuf, reinterpret_cast<const uint8_t*>(s.d_hash), s.pin_hash_dev,
+                        static_cast<size_t>(n) * sh.rows * sizeof(int32_t));
             }
-        } else if (sh.direct) {
-            Dma dma(hipMemcpyHostToDevice, s.stream);
-            for (int q = 0; q < n; ++q)
-                for (int j = 0; j < sh.cols; ++j) {
-                    const size_t i = static_cast<size_t>(q) * kern::kMaxCols + j;
-                    const size_t nb = d.src_n[i], lo = d.src_lo[i], hi = d.src_hi[i];
-                    uint8_t* const dev = s.d_in + q * in_stride + j * sh.pitch;
-                    const uint8_t* const pin = s.pin_in + q * in_stride + j * sh.pitch;
-                    dma.add(dev, pin, lo);
-                    dma.add(dev + lo, d.src[i] + lo, hi - lo);
-                    dma.add(dev + hi, pin + hi, nb - hi);
-                }
-            e = dma.flush();
-        } else {
-            e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
+            begin[k] = np;
+            if (!room || np + gbuf.size() + sbuf.size() > s.max_pieces) return false;
+            // interleave: piece i of a list of m sits at position (i + 0.5) / m of the stage
+            size_t gi = 0, si = 0;
+            const size_t ng = gbuf.size(), ns = sbuf.size();
+            while (gi < ng || si < ns) {
+                const bool take_g = si == ns || (gi < ng && (2 * gi + 1) * ns <= (2 * si + 1) * ng);
+                s.pieces[np++] = take_g ? gbuf[gi++] : sbuf[si++];
+            }
         }
+        begin[st.n + 1] = np;
+        return true;
+    }
+
+    // Direct batches: each unit's [lo, hi) straight from / to its caller's
+    // page-locked memory (a locked pageable unit's interior pages, or a pool
+    // unit), the rest (a locked unit's partial end pages) through the arena; by
+    // gather / scatter kernels reading the piece table where it lies.  s's
+    // buffers, stream and events never change after init(); its shape comes from
+    // the copy taken under mu_.
+    hipError_t issue_direct(Slab& s, const Shape& sh, int n, const DirectSlots& d)
+    {
+        Steps st = plan_steps(sh, n, d);
+        size_t begin[kMaxSteps + 2];
+        if (!write_pieces(s, sh, n, d, st, begin, gbuf_, sbuf_)) {
+            st = Steps{1, sh.len, kern::kMaxPieceBytes};  // one step of 64 KiB pieces always fits
+            if (!write_pieces(s, sh, n, d, st, begin, gbuf_, sbuf_)) return hipErrorInvalidValue;
+        }
+        const size_t in_stride = sh.cols * sh.pitch, out_stride = sh.rows * sh.pitch;
+        if (sh.padded)  // [step][slot][col]: each window's share of every unit's content
+            for (int t = 0; t < st.n; ++t) {
+                const size_t w0 = t * st.window, w = std::min(sh.len, w0 + st.window) - w0;
+                uint32_t* l = s.pin_lens + static_cast<size_t>(t) * n * sh.cols;
+                for (int q = 0; q < n; ++q)
+                    for (int j = 0; j < sh.cols; ++j) {
+                        const size_t raw = d.src_n[static_cast<size_t>(q) * kern::kMaxCols + j];
+                        l[q * sh.cols + j] = static_cast<uint32_t>(raw > w0 ? std::min(raw - w0, w) : 0);
+                    }
+            }
+        hipError_t e = hipSuccess;
+        const bool seed = sh.hashed && st.n > 1;  // windows add into entries seeded 31^len
+        if (seed)
+            e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_hash), static_cast<int>(kern::pow31(sh.len)),
+                                  static_cast<size_t>(n) * sh.rows, s.stream);
+        for (int k = 0; k <= st.n && e == hipSuccess; ++k) {
+            e = kern::launch_copy_pieces(s.pieces_dev + begin[k], static_cast<uint32_t>(begin[k + 1] - begin[k]), s.stream);
+            // the gate: the batch's last gather is done (the next batch's gathers may start beside its last scatter)
+            if (e == hipSuccess && k == st.n - 1) e = hipEventRecord(s.h2d_done, s.stream);
+            if (e != hipSuccess || k == st.n) break;
+            const size_t w0 = k * st.window, w = std::min(sh.len, w0 + st.window) - w0;
+            ApplyParams p;
+            p.len = w;
+            p.stripes = static_cast<uint64_t>(n);
+            p.cols = sh.cols;
+            p.rows = sh.rows;
+            for (int j = 0; j < sh.cols; ++j) p.src[j] = col(s.d_in, in_stride, j * sh.pitch + w0);
+            for (int r = 0; r < sh.rows; ++r) p.dst[r] = col(s.d_out, out_stride, r * sh.pitch + w0);
+            std::memcpy(p.coef, sh.coef, sizeof(p.coef));
+            if (sh.padded) {
+                p.padded = true;
+                p.lens = s.d_lens + static_cast<size_t>(k) * n * sh.cols;
+            } else if (w % 16) {  // the unit's last partial segment, in the same launch
+                p.padded = true;
+                for (int j = 0; j < sh.cols; ++j) p.clen[j] = static_cast<uint32_t>(w);
+            }
+            if (sh.hashed) {
+                p.hashes = s.d_hash;
+                p.hash_stride = static_cast<uint32_t>(sh.rows);
+                p.hash_base = w0;
+                p.hash_seed = !seed;
+                p.hash_scratch = s.d_scratch;
+                p.hash_scratch_words = s.scratch_words;
+            }
+            e = kern::launch_apply(p, s.stream);
+        }
+        if (e == hipSuccess) e = hipEventRecord(s.done_ev, s.stream);
+        return e;
+    }
+
+    // Staged batches (the callers copied their units into the pinned arena): one
+    // H2D, one coding launch over the arena's tiles, one D2H.
+    hipError_t issue_staged(Slab& s, const Shape& sh, int n)
+    {
+        const size_t in_stride = sh.tiles * sh.cols * sh.pitch;  // per slot
+        const size_t out_stride = sh.tiles * sh.rows * sh.pitch;
+        hipError_t e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
         if (e == hipSuccess && sh.padded)
             e = hipMemcpyAsync(s.d_lens, s.pin_lens, static_cast<size_t>(n) * sh.cols * sizeof(uint32_t),
                                hipMemcpyHostToDevice, s.stream);
         if (e == hipSuccess) e = hipEventRecord(s.h2d_done, s.stream);
-        if (e == hipSuccess && wait_mode() == kWaitCallback) e = hipLaunchHostFunc(s.stream, &Batcher::on_h2d, &s);
         if (e == hipSuccess) {
             // coding stripes: the slots' tiles in order (untiled: the slots)
             ApplyParams p;
@@ -1688,91 +1834,26 @@ private:
             }
             e = kern::launch_apply(p, s.stream);
         }
-        if (e == hipSuccess && sh.direct && by_kernel) {
-            e = kern::launch_copy_pieces(s.pieces_dev + gather_n, static_cast<uint32_t>(scatter_n), s.stream);
-        } else if (e == hipSuccess && sh.direct) {
-            Dma dma(hipMemcpyDeviceToHost, s.stream);
-            for (int q = 0; q < n; ++q)
-                for (int r = 0; r < sh.rows; ++r) {
-                    const size_t i = static_cast<size_t>(q) * kern::kMaxRows + r;
-                    const size_t lo = d.dst_lo[i], hi = d.dst_hi[i];
-                    const uint8_t* const dev = s.d_out + q * out_stride + r * sh.pitch;
-                    uint8_t* const pin = s.pin_out + q * out_stride + r * sh.pitch;
-                    dma.add(pin, dev, lo);
-                    dma.add(d.dst[i] + lo, dev + lo, hi - lo);
-                    dma.add(pin + hi, dev + hi, sh.len - hi);
-                }
-            e = dma.flush();
-        } else if (e == hipSuccess) {
-            e = hipMemcpyAsync(s.pin_out, s.d_out, n * out_stride, hipMemcpyDeviceToHost, s.stream);
-        }
+        if (e == hipSuccess) e = hipMemcpyAsync(s.pin_out, s.d_out, n * out_stride, hipMemcpyDeviceToHost, s.stream);
         if (e == hipSuccess && sh.hashed)
             e = hipMemcpyAsync(s.pin_hash, s.d_hash, static_cast<size_t>(n) * sh.rows * sizeof(int32_t),
                                hipMemcpyDeviceToHost, s.stream);
-        if (e == hipSuccess)
-            e = wait_mode() == kWaitPoll ? hipEventRecord(s.done_ev, s.stream) : hipLaunchHostFunc(s.stream, &Batcher::on_done, &s);
+        if (e == hipSuccess) e = hipEventRecord(s.done_ev, s.stream);
         return e;
     }
 
-    // hipMemcpyAsync calls of one direction, a piece contiguous on both sides with
-    // the previous one extending it.  The first error stops the issue.
-    struct Dma {
-        hipMemcpyKind kind;
-        hipStream_t stream;
-        uint8_t* dst = nullptr;
-        const uint8_t* src = nullptr;
-        size_t n = 0;
-        hipError_t e = hipSuccess;
-        Dma(hipMemcpyKind k, hipStream_t s) : kind(k), stream(s) {}
-        void add(void* to, const void* from, size_t bytes)
-        {
-            if (!bytes || e != hipSuccess) return;
-            auto* t = static_cast<uint8_t*>(to);
-            auto* f = static_cast<const uint8_t*>(from);
-            if (n && t == dst + n && f == src + n) {
-                n += bytes;
-                return;
-            }
-            (void)flush();
-            dst = t;
-            src = f;
-            n = bytes;
-        }
-        hipError_t flush()
-        {
-            if (n && e == hipSuccess) e = hipMemcpyAsync(dst, src, n, kind, stream);
-            n = 0;
-            return e;
-        }
-    };
-
-    // How the dispatcher learns that a batch's inputs have landed (self-clocking)
-    // and the callers that their batch is done (ELECT_EC_DISPATCH_WAIT):
-    //  - poll (the default): a poller thread per device queries the batches'
-    //    events (hipEventQuery) and sleeps ELECT_EC_POLL_US (default 25) between
-    //    rounds;
-    //  - callback: host-function callbacks behind the H2D and behind the batch
-    //    (hipLaunchHostFunc);
-    //  - event: the dispatcher waits in hipEventSynchronize, completions by callback.
-    // Every waiting primitive of this HIP runtime spins a core for as long as the
-    // device work it waits for runs: hipStreamSynchronize, hipEventSynchronize
-    // (hipEventBlockingSync events too) 94 % of a core each behind 5 ms kernels,
-    // the runtime's host-function thread 96 % (tools/tune/spin_probe.cpp,
-    // profiles/r05/spin_probe.txt), where hipEventQuery every 50 us costs 2 %.  At
-    // 64 callers the callback thread alone was 19-20 core-ms per GiB, the largest
-    // single cost of the host path (tools/hostpath_cbench per-thread CPU).  The
-    // event mode first spun the dispatcher too (round 5 before callbacks: 53
-    // against 35 core-ms per GiB, hostpath_register_ab.txt E).
-    enum WaitMode { kWaitPoll, kWaitCallback, kWaitEvent };
-    static WaitMode wait_mode()
-    {
-        static const WaitMode m = [] {
-            const char* e = std::getenv("ELECT_EC_DISPATCH_WAIT");
-            const std::string v = e ? e : "";
-            return v == "event" ? kWaitEvent : v == "callback" ? kWaitCallback : kWaitPoll;
-        }();
-        return m;
-    }
+    // How the dispatcher learns that a batch has passed its gate (self-clocking)
+    // and the callers that their batch is done: a poller thread per device
+    // queries the batches' events (hipEventQuery) and sleeps ELECT_EC_POLL_US
+    // (default 25) between rounds.  Every waiting primitive of this HIP runtime
+    // spins a core for as long as the device work it waits for runs:
+    // hipStreamSynchronize, hipEventSynchronize (hipEventBlockingSync events too)
+    // 94 % of a core each behind 5 ms kernels, the runtime's host-function thread
+    // 96 % (tools/tune/spin_probe.cpp, profiles/r05/spin_probe.txt), where
+    // hipEventQuery every 50 us costs 2 %.  At 64 callers the callback thread
+    // alone was 19-20 core-ms per GiB, and the dispatcher spinning on the H2D
+    // event 53 against 35 (hostpath_register_ab.txt E); both modes were A/B
+    // switches in round 5 (ELECT_EC_DISPATCH_WAIT) and are gone since.
     static unsigned poll_us()
     {
         static const unsigned u = [] {
@@ -1782,8 +1863,8 @@ private:
         return u;
     }
 
-    // Poll mode: marks in-flight batches' inputs landed (waking the dispatcher)
-    // and finishes completed batches (waking their callers).  Only this thread
+    // Marks in-flight batches past their gate (waking the dispatcher) and
+    // finishes completed batches (waking their callers).  Only this thread
     // finishes an issued batch, so a batch it saw issued stays in flight until
     // it finishes it.
     void poller()
@@ -1801,21 +1882,21 @@ private:
                 if (x.state != Slab::kInFlight || !x.issued) continue;
                 const bool landed = x.h2d_landed;
                 lock.unlock();  // (a slab's events never change after init)
-                // the batch cannot be done before its inputs have landed
+                // the batch cannot be done before it has passed its gate
                 const hipError_t eh = landed ? hipSuccess : hipEventQuery(x.h2d_done);
                 const hipError_t ed = eh == hipSuccess ? hipEventQuery(x.done_ev) : hipErrorNotReady;
+                const bool failed = (eh != hipSuccess && eh != hipErrorNotReady) || (ed != hipSuccess && ed != hipErrorNotReady);
+                if (failed) drain(x);  // nothing of the batch may still run when its callers return
                 lock.lock();
                 if (!landed && eh != hipErrorNotReady) {
                     x.h2d_landed = true;
                     cv_worker_.notify_one();
                 }
                 if (eh != hipSuccess && eh != hipErrorNotReady) {  // a failed batch is done, with its error
-                    (void)hipGetLastError();
                     finish(&x, map_hip(eh));
                     continue;
                 }
                 if (ed == hipErrorNotReady) continue;
-                if (ed != hipSuccess) (void)hipGetLastError();
                 finish(&x, ed == hipSuccess ? ELECT_EC_OK : map_hip(ed));
             }
             lock.unlock();
@@ -1824,23 +1905,10 @@ private:
         }
     }
 
-    static void on_h2d(void* arg)  // HIP host-function callback: no HIP calls in here
-    {
-        Slab* s = static_cast<Slab*>(arg);
-        std::lock_guard<std::mutex> lock(s->owner->mu_);
-        s->h2d_landed = true;
-        s->owner->cv_worker_.notify_one();
-    }
-
-    static void on_done(void* arg)  // HIP host-function callback: no HIP calls in here
-    {
-        Slab* s = static_cast<Slab*>(arg);
-        std::lock_guard<std::mutex> lock(s->owner->mu_);
-        s->owner->finish(s, ELECT_EC_OK);
-    }
-
     void finish(Slab* s, int status)  // mu_ held
     {
+        s->t_finish = now_ns();
+        add_phase(4, s->t_issue1, s->t_finish);
         s->status = status;
         s->issued = false;
         if (s->readers == 0) {
@@ -1859,8 +1927,9 @@ private:
     // every reservation: O(callers^2) wake-ups per batch at 64 callers).
     std::mutex mu_;
     std::condition_variable cv_worker_;  // the dispatcher
-    std::condition_variable cv_poll_;    // the poller (poll mode), while no batch is in flight
+    std::condition_variable cv_poll_;    // the poller, while no batch is in flight
     DirectSlots slots_;                  // the dispatcher's copy of a direct batch's slots (its thread only)
+    std::vector<kern::CopyPiece> gbuf_, sbuf_;  // a stage's gather / scatter pieces (dispatcher thread only)
     std::condition_variable cv_slot_;    // callers waiting for an arena to reserve in
     bool started_ = false;
     bool init_failed_ = false;  // the arenas could not be allocated: every call runs directly
@@ -1932,13 +2001,17 @@ struct ZeroCopy {
     }
 
     // Page-aligned, merged [begin, end) intervals covering every byte the
-    // call's kernels touch (inputs: input_span).
+    // call's kernels touch (inputs: input_span), pool units left out: the pool
+    // holds them locked already and the kernel addresses them at the pool's
+    // device address (locking them again here, and unlocking after the
+    // call, would have released pages the pool still owns).
     static std::vector<std::pair<uintptr_t, uintptr_t>> ranges(const HostOp& op, size_t len)
     {
         constexpr uintptr_t kPage = 4096;
+        PinnedPool& pool = PinnedPool::get();
         std::vector<std::pair<uintptr_t, uintptr_t>> r;
         auto add = [&](const void* p, size_t n) {
-            if (!p || !n) return;
+            if (!p || !n || pool.pinned(p, n)) return;
             const uintptr_t a = reinterpret_cast<uintptr_t>(p);
             r.emplace_back(a & ~(kPage - 1), (a + n + kPage - 1) & ~(kPage - 1));
         };
@@ -1967,12 +2040,14 @@ struct ZeroCopy {
             (void)hipGetLastError();
             return e == hipSuccess && a.type == hipMemoryTypeUnregistered;
         };
+        PinnedPool& pool = PinnedPool::get();
         for (int j = 0; j < op.cols; ++j) {
             const size_t n = input_span(op, j, len);
-            if (op.in[j] && n && !(unknown(op.in[j]) && unknown(op.in[j] + n - 1))) return false;
+            if (op.in[j] && n && !pool.pinned(op.in[j], n) && !(unknown(op.in[j]) && unknown(op.in[j] + n - 1)))
+                return false;
         }
         for (int r = 0; r < op.rows; ++r)
-            if (!(unknown(op.out[r]) && unknown(op.out[r] + len - 1))) return false;
+            if (!pool.pinned(op.out[r], len) && !(unknown(op.out[r]) && unknown(op.out[r] + len - 1))) return false;
         return true;
     }
 
@@ -2036,9 +2111,9 @@ struct ZeroCopy {
             p.rows = op.rows;
             std::memcpy(p.coef, op.coef, sizeof(p.coef));
             PinnedPool& pool = PinnedPool::get();
-            auto device_of = [&](const void* x) -> const void* {  // x inside one locked range (or the pool)
+            auto device_of = [&](const void* x, size_t n) -> const void* {  // inside the pool or one locked range
                 const uintptr_t a = reinterpret_cast<uintptr_t>(x);
-                if (pinned) return reinterpret_cast<const void*>(pool.device_addr(x));
+                if (pinned || pool.pinned(x, n)) return reinterpret_cast<const void*>(pool.device_addr(x));
                 for (size_t i = 0; i < rs.size(); ++i)
                     if (a >= rs[i].first && a < rs[i].second)
                         return reinterpret_cast<const void*>(dev_lo[i] + (a - rs[i].first));
@@ -2047,11 +2122,11 @@ struct ZeroCopy {
             bool ok = true;
             for (int j = 0; j < op.cols && ok; ++j) {
                 const void* d = nullptr;
-                if (op.in[j] && (!op.lens || op.lens[j])) ok = (d = device_of(op.in[j])) != nullptr;
+                if (op.in[j] && (!op.lens || op.lens[j])) ok = (d = device_of(op.in[j], input_span(op, j, len))) != nullptr;
                 p.src[j] = col(d, 0, 0);
             }
             for (int q = 0; q < op.rows && ok; ++q) {
-                const void* d = device_of(op.out[q]);
+                const void* d = device_of(op.out[q], len);
                 ok = d != nullptr;
                 p.dst[q] = col(d, 0, 0);
             }
@@ -2103,7 +2178,7 @@ bool lone_caller(int dev)
 // units registered for the call (ELECT_EC_REGISTER=1), registration attempts that fell back
 // to staging (no free slot, or a range refused), failed unregistrations (entry 7 is read from
 // g_unregister_failures), CPU ns registering / unregistering / issuing batches (8-10).
-constexpr int kStats = 11;
+constexpr int kStats = 19;
 std::atomic<uint64_t> g_stats[kStats];
 
 }  // namespace
@@ -2111,6 +2186,7 @@ std::atomic<uint64_t> g_stats[kStats];
 int run_host(const HostOp& op, size_t len)
 {
     if (len == 0) return ELECT_EC_OK;  // JEC/ErasureEncoder.java:41-44, JEC/ErasureDecoder.java:36-38
+    const int64_t t_enter = now_ns();
     for (int j = 0; j < op.cols; ++j) {
         if (op.lens && op.lens[j] > len) return ELECT_EC_EINVAL;
         if (!op.in[j] && !(op.lens && op.lens[j] == 0)) return ELECT_EC_EINVAL;
@@ -2139,7 +2215,7 @@ int run_host(const HostOp& op, size_t len)
     } in_flight(g_in_flight[dev]);
     try {  // nothing may unwind into the JVM: allocation failures become status codes
         rc = Batcher::kFallback;
-        // units in page-locked pool buffers (elect_ec_host_alloc) move by DMA with no
+        // units in page-locked pool buffers (elect_ec_host_alloc) move by kernels with no
         // staging copy (batched); any other lone caller's may be page-locked for the call
         const bool direct = direct_op(op, len);
         if (ZeroCopy::eligible(op, len, in_flight.now, lone_caller(dev))) {
@@ -2167,9 +2243,15 @@ int run_host(const HostOp& op, size_t len)
                 registered = RegisterPath::plan(op, len, dev, plan);
                 if (!registered) g_stats[6].fetch_add(1);
             }
+            t_phase_mark = now_ns();
+            add_phase(0, t_enter, t_phase_mark);
             struct Release {  // the registrations outlive the call's batch, not the call
                 DirectPlan& p;
-                ~Release() { RegisterPath::release(p); }
+                ~Release()
+                {
+                    RegisterPath::release(p);
+                    add_phase(6, t_phase_mark, now_ns());
+                }
             } release{plan};
             rc = b ? b->submit(op, len, &plan) : ELECT_EC_ENOMEM;
             if (rc != Batcher::kFallback) g_stats[registered ? 5 : direct ? 4 : 2].fetch_add(1);
@@ -2218,6 +2300,8 @@ int host_path_stats(uint64_t* out, int n)
     g_stats[8].store(g_register_cpu_ns.load());
     g_stats[9].store(g_unregister_cpu_ns.load());
     g_stats[10].store(g_issue_cpu_ns.load());
+    for (int i = 0; i < 7; ++i) g_stats[11 + i].store(g_phase_ns[i].load());
+    g_stats[18].store(g_batches.load());
     for (int i = 0; i < w; ++i) out[i] = g_stats[i].load();
     return w;
 }

@@ -479,8 +479,13 @@ hipError_t hbm_probe(int kind, const void* src, void* dst, size_t bytes, int blo
 template <bool VEC, bool NT, int U>
 __global__ __launch_bounds__(kBlock) void copy_pieces_kernel(const CopyPiece* __restrict__ pieces, uint32_t n)
 {
+  // The piece table lies in page-locked host memory: the block's next descriptor
+  // is read while this piece's data moves, so its PCIe round trip is not paid
+  // between pieces (round 6: 16 KiB pieces for pipelined steps).
+  CopyPiece next = blockIdx.x < n ? pieces[blockIdx.x] : CopyPiece{};
   for (uint32_t pi = blockIdx.x; pi < n; pi += gridDim.x) {
-    const CopyPiece pc = pieces[pi];
+    const CopyPiece pc = next;
+    if (pi + gridDim.x < n) next = pieces[pi + gridDim.x];
     const uint32_t vecs = VEC ? pc.n / 16 : 0;
     uint32_t v = threadIdx.x;
     // U loads in flight per lane before their stores

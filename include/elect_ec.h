@@ -150,7 +150,12 @@ int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes);
  * another extent), out[7] unlock failures (hsa_amd_memory_unlock; 0 unless the
  * runtime's locks were disturbed by another party), out[8..10] CPU time in ns
  * spent registering, unregistering, and issuing batches in the dispatcher
- * threads.  Writes min(n, 11) entries; returns the count. */
+ * threads, out[11..17] wall time in ns of the batched calls' phases, summed
+ * over calls (locking the units; copying arena edges and joining a batch;
+ * waiting for the batch's issue; the issue, per batch; issue end to the
+ * poller seeing the batch done, per batch; done to the caller awake; awake to
+ * return, edges out and unlocks), out[18] batches issued.  Writes min(n, 19)
+ * entries; returns the count. */
 int elect_ec_host_path_stats(uint64_t* out, int n);
 
 /* Page-locked host memory for the units of host-memory calls.  ELECT allocates

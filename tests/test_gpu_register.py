@@ -118,14 +118,14 @@ print("BAD " + "; ".join(errors[:6]) if errors else "OK", json.dumps(stats))
 """
 
 
-# The batcher's completion mechanisms (Batcher::wait_mode): the poller (default),
-# host-function callbacks, and the dispatcher in hipEventSynchronize (A/B modes).
-@pytest.mark.parametrize("wait", ["poll", "callback", "event"])
-def test_registered_units_back_to_back_then_device_work(wait):
+# Direct batches in one step (round 5's unpipelined batch) and pipelined over
+# windows (round 6, Batcher::issue_direct; 256 KiB steps put four windows in
+# each 1 MiB unit, so window edges fall inside the units' locked interiors).
+@pytest.mark.parametrize("steps", ["1", "8"])
+def test_registered_units_back_to_back_then_device_work(steps):
     code = SCRIPT.replace("ROOT", repr(ROOT))
     env = dict(os.environ, ELECT_EC_REGISTER="1", ELECT_EC_REGISTER_SLOTS="4", ELECT_EC_ZEROCOPY="0",
-               ELECT_EC_DISPATCH_WAIT=wait)
-    env.pop("ELECT_EC_DIRECT_MOVE", None)
+               ELECT_EC_PIPELINE_STEPS=steps, ELECT_EC_STEP_KB="256")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0 and r.stdout.strip().startswith("OK"), r.stdout[-3000:] + r.stderr[-3000:]
     st = json.loads(r.stdout.strip().split(" ", 1)[1])

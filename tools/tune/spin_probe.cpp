@@ -13,13 +13,23 @@
 //   longk_sync      the same with hipStreamSynchronize from 3 threads instead of host functions
 //   longk_blocking  ... hipEventRecord + hipEventSynchronize on a hipEventBlockingSync event, 3 threads
 //   longk_poll      ... hipEventRecord, then hipEventQuery every 50 us (sleeping between), 3 threads
+// Round 6, cross-stream chains (the host path's gather -> code -> scatter streams), 150 per s of
+// a 5 ms kernel on stream 0, then a 1 ms kernel on stream 1, then a 1 ms kernel on stream 2, each
+// after the previous, the host polling the last with hipEventQuery every 50 us:
+//   chain_same       all three on stream 0 (no cross-stream dependency: round 5's pattern)
+//   chain_event      hipEventRecord + hipStreamWaitEvent between streams (hipEventDisableTiming)
+//   chain_event_nf   ... events also hipEventDisableSystemFence
+//   chain_event_dev  ... events also hipEventReleaseToDevice
+//   chain_value      hipStreamWriteValue32 of a device flag behind each kernel, hipStreamWaitValue32 on the next stream
 //
-//   hipcc -O2 -std=c++17 tools/tune/spin_probe.cpp -L/opt/rocm/lib -lhsa-runtime64 -pthread -o tools/tune/spin_probe
+//   hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/tune/spin_probe.cpp -L/opt/rocm/lib -lhsa-runtime64 -pthread -o tools/tune/spin_probe
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
 #include <dirent.h>
+#include <execinfo.h>
+#include <signal.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -75,9 +85,20 @@ static std::map<long, double> thread_cpu(std::map<long, std::string>* names)
 
 static void noop(void*) {}
 
+static void on_segv(int sig)
+{
+    void* bt[64];
+    const int n = backtrace(bt, 64);
+    std::fprintf(stderr, "signal %d, backtrace:\n", sig);
+    backtrace_symbols_fd(bt, n, 2);
+    std::_Exit(128 + sig);
+}
+
 int main(int argc, char** argv)
 {
+    signal(SIGSEGV, on_segv);
     const std::string mode = argc > 1 ? argv[1] : "idle";
+    std::fprintf(stderr, "mode %s\n", mode.c_str());
     const double secs = 2.0;
     hipStream_t s;
     if (hipStreamCreate(&s) != hipSuccess) return 2;
@@ -156,6 +177,33 @@ int main(int argc, char** argv)
                 hipLaunchKernelGGL(wait_kernel, dim3(1), dim3(64), 0, st[q], uint64_t{100000});
                 (void)hipLaunchHostFunc(st[q], noop, nullptr);
             }
+        } else if (mode.rfind("chain_", 0) == 0) {
+            static hipEvent_t ev[3];
+            static uint32_t* flag = nullptr;
+            static uint32_t seq = 0;
+            if (!ev[0]) {
+                const unsigned f = hipEventDisableTiming | (mode == "chain_event_nf" ? hipEventDisableSystemFence : 0u) |
+                                   (mode == "chain_event_dev" ? hipEventReleaseToDevice : 0u);
+                for (auto& e : ev) (void)hipEventCreateWithFlags(&e, f);
+                (void)hipMalloc(reinterpret_cast<void**>(&flag), 2 * sizeof(uint32_t));
+                (void)hipMemset(flag, 0, 2 * sizeof(uint32_t));
+            }
+            const bool same = mode == "chain_same", value = mode == "chain_value";
+            ++seq;
+            const uint64_t ticks[3] = {500000, 100000, 100000};
+            for (int q = 0; q < 3; ++q) {
+                hipStream_t x = same ? st[0] : st[q];
+                if (q > 0 && !same) {
+                    if (value)
+                        (void)hipStreamWaitValue32(x, flag + q - 1, seq, hipStreamWaitValueGte, 0xFFFFFFFFu);
+                    else
+                        (void)hipStreamWaitEvent(x, ev[q - 1], 0);
+                }
+                hipLaunchKernelGGL(wait_kernel, dim3(1), dim3(64), 0, x, ticks[q]);
+                if (value && q < 2) (void)hipStreamWriteValue32(x, flag + q, seq, 0);
+                (void)hipEventRecord(ev[q], x);
+            }
+            while (hipEventQuery(ev[2]) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(50));
         } else if (mode == "hsa_lock") {
             void* ap = nullptr;
             if (hsa_amd_memory_lock(host.data() + 4096 - (reinterpret_cast<uintptr_t>(host.data()) & 4095), 2 << 20, &gpu,
@@ -165,6 +213,7 @@ int main(int argc, char** argv)
         ++iters;
         std::this_thread::sleep_for(std::chrono::microseconds(mode == "hostfunc_burst"   ? 6667
                                                               : mode == "longk_hostfunc" ? 6000
+                                                              : mode.rfind("chain_", 0) == 0 ? 100
                                                               : 500));
     }
     const auto t1 = thread_cpu(&names);
