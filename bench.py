@@ -169,6 +169,9 @@ def parse():
                     help="hostpath: repeat the timed calls until at least this much wall time has passed")
     ap.add_argument("--no-hostpath", action="store_true",
                     help="headline: skip the JNI-convention host path over all the job's devices")
+    ap.add_argument("--host-numa", choices=("none", "local", "remote"), default="none",
+                    help="hostpath: bind the process (callers, their buffers by first touch, the library's "
+                         "threads) to the device's NUMA node (local) or another node (remote) before allocating")
     ap.add_argument("--host-alloc", choices=("pageable", "pinned"), default="pageable",
                     help="hostpath: the callers' buffers are ordinary memory (ELECT's ByteBuffer.allocateDirect), or "
                          "elect_ec_host_alloc buffers (page-locked; the batcher then moves them by DMA, no staging "
@@ -1015,6 +1018,17 @@ def config_hostpath(args, world, rank, dev):
         if ndev > avail:
             raise SystemExit(f"--host-devices {ndev}: only {avail} device(s) visible")
         _lib.set_host_devices(list(range(ndev)))
+    numa = {"policy": args.host_numa}
+    if args.host_numa != "none":  # before any buffer is touched: first-touch places them on the bound node
+        nodes = numa_cpus()
+        gnode = _lib.device_numa_node(dev.index if dev.index is not None else 0)
+        numa["gpu_node"] = gnode
+        if gnode in nodes and len(nodes) >= 2:
+            target = gnode if args.host_numa == "local" else min(n for n in nodes if n != gnode)
+            os.sched_setaffinity(0, set(nodes[target]))
+            numa.update(bound_node=target, cpus=len(nodes[target]))
+        else:
+            numa["unavailable"] = f"device node {gnode}, nodes {sorted(nodes)}"
     bufs, keep = [], []
     pinned = args.host_alloc == "pinned"
 
@@ -1147,7 +1161,7 @@ def config_hostpath(args, world, rank, dev):
     quota = host_cpu_info()["quota_cores"] or len(os.sched_getaffinity(0))
     return {"metric": f"GiB/s host-memory RS(6,4) {op_name} through the C ABI (JNI calling convention)",
             "value": round(data_gib / dt, 2), "unit": "GiB/s", "n_gpus": world,
-            "devices": ndev, "callers": T, "host_path_stats": stats, "host_alloc": args.host_alloc,
+            "devices": ndev, "callers": T, "host_path_stats": stats, "host_alloc": args.host_alloc, "numa": numa,
             "host_register": os.environ.get("ELECT_EC_REGISTER", "library default"),
             # CPU time the whole process spent (every caller, helper and dispatcher thread) per GiB
             # of data coded: what the offload costs the node's cores

@@ -75,6 +75,8 @@ SIGNATURES = [
     ("elect_ec_unaligned_vector_ok", ctypes.c_int, [_ip]),
     ("elect_ec_hbm_probe", ctypes.c_int, [ctypes.c_int, _cp, _cp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, _cp]),
     ("elect_ec_set_host_devices", ctypes.c_int, [_ip, ctypes.c_int]),
+    ("elect_ec_device_numa_node", ctypes.c_int, [ctypes.c_int, _ip]),
+    ("elect_ec_host_device_map", ctypes.c_int, [_ip, _ip, ctypes.c_int, _ip, ctypes.c_int, _ip]),
     ("elect_ec_set_batching", ctypes.c_int, [ctypes.c_int, ctypes.c_uint, ctypes.c_size_t]),
     ("elect_ec_host_path_stats", ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     ("elect_ec_mix_probe", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
@@ -238,6 +240,23 @@ def set_host_devices(devices) -> None:
 def set_batching(enable: bool, window_us: int = 0, arena_bytes: int = 256 << 20) -> None:
     """Cross-thread batching of concurrent host-memory encodes/decodes of one shape."""
     check(lib.elect_ec_set_batching(int(enable), window_us, arena_bytes), "set_batching")
+
+
+def device_numa_node(device: int) -> int:
+    """NUMA node of a HIP device (elect_ec_device_numa_node; -1 unknown)."""
+    n = ctypes.c_int(-1)
+    check(lib.elect_ec_device_numa_node(device, ctypes.byref(n)), "device_numa_node")
+    return n.value
+
+
+def host_device_map(devices, device_nodes, thread_nodes) -> list:
+    """The devices threads on thread_nodes would get from devices on device_nodes,
+    in that order (elect_ec_host_device_map: the library's NUMA-aware choice)."""
+    out = (ctypes.c_int * max(1, len(thread_nodes)))()
+    check(lib.elect_ec_host_device_map(int_array(devices), int_array(device_nodes), len(devices),
+                                       int_array(thread_nodes) if thread_nodes else None, len(thread_nodes), out),
+          "host_device_map")
+    return list(out[:len(thread_nodes)])
 
 
 def host_path_stats() -> dict:

@@ -306,6 +306,25 @@ int elect_ec_device_count(int* count)
 
 int elect_ec_set_host_devices(const int* devices, int n) { return elect::host::set_host_devices(devices, n); }
 
+int elect_ec_device_numa_node(int device, int* node)
+{
+    if (!node) return ELECT_EC_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        (void)hipGetLastError();
+        return ELECT_EC_ENODEV;
+    }
+    if (device < 0 || device >= ndev) return ELECT_EC_EINVAL;
+    *node = elect::host::device_numa_node(device);
+    return ELECT_EC_OK;
+}
+
+int elect_ec_host_device_map(const int* devices, const int* device_nodes, int num_devices, const int* thread_nodes,
+                             int num_threads, int* out)
+{
+    return elect::host::host_device_map(devices, device_nodes, num_devices, thread_nodes, num_threads, out);
+}
+
 int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes)
 {
     return elect::host::set_batching(enable, window_us, arena_bytes);

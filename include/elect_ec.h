@@ -120,6 +120,22 @@ int elect_ec_mix_probe(int num_in, int num_out, size_t chunk_size, size_t num_st
  * n = 0 restores the default.  Returns ELECT_EC_EINVAL for an unknown device. */
 int elect_ec_set_host_devices(const int* devices, int n);
 
+/* NUMA placement of the host-memory calls (round 6).  With a device list, a
+ * calling thread is assigned, on its first call, a device of the list on its
+ * own NUMA node (the node it runs on then, getcpu), round robin among those;
+ * a thread on a node with no listed device takes the next of the whole list.
+ * ELECT's coding threads allocate and fill their units themselves
+ * (ECMessageVerbHandler.java:298-314), so with first-touch placement a GPU on
+ * the thread's node reads them without crossing the socket link.
+ * ELECT_EC_NUMA=0 turns it off (plain round robin).
+ * elect_ec_device_numa_node: the node of a HIP device (its PCI function's
+ * sysfs numa_node; -1 unknown).  elect_ec_host_device_map (diagnostics, no
+ * device needed): the devices that threads on thread_nodes[0..num_threads)
+ * would get, in that order, from devices[] on device_nodes[]. */
+int elect_ec_device_numa_node(int device, int* node);
+int elect_ec_host_device_map(const int* devices, const int* device_nodes, int num_devices, const int* thread_nodes,
+                             int num_threads, int* out);
+
 /* Cross-thread batching of host-memory calls (on by default; ELECT_EC_BATCH=0
  * turns it off; ELECT_EC_BATCH_WINDOW_US, ELECT_EC_BATCH_ARENA_MB).  While
  * on, concurrent elect_ec_encode / elect_ec_decode calls of the same shape share

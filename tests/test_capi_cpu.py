@@ -276,3 +276,30 @@ def test_host_alloc_pool_semantics():
     owner = arr.base.obj._owner if hasattr(arr.base, "obj") else None
     assert owner is not None and owner.addr and _lib.lib.elect_ec_host_free(owner.addr) == 0
     owner.addr = 0  # freed here by hand; its close() is then a no-op
+
+
+def test_numa_device_map():
+    """elect_ec_host_device_map: the device each calling thread gets (host_device's
+    NUMA-aware round robin, host_path.cpp numa_pick), no device needed.  ELECT's
+    64 coding threads on a node of 8 GPUs, 4 per socket (the GPU boxes' layout,
+    profiles/r06/numa_facts.txt)."""
+    from elect_amd import _lib
+    devs, nodes = list(range(8)), [0, 0, 0, 0, 1, 1, 1, 1]
+    threads = [t % 2 for t in range(64)]  # alternating sockets
+    got = _lib.host_device_map(devs, nodes, threads)
+    for t, d in enumerate(got):
+        assert nodes[d] == threads[t], (t, d)  # every thread on a GPU of its own socket
+    for n in (0, 1):  # round robin within the node: each local GPU 8 threads
+        mine = [d for d, x in zip(got, threads) if x == n]
+        assert mine[:4] == [4 * n + i for i in range(4)]
+        assert sorted(mine.count(d) for d in set(mine)) == [8, 8, 8, 8]
+    # a node without a listed GPU, or an unknown node, falls back to round robin over the whole list
+    assert _lib.host_device_map(devs, nodes, [2, 2, 2, -1, -1]) == [0, 1, 2, 3, 4]
+    # devices of unknown node (sysfs without NUMA info): plain round robin for every thread
+    assert _lib.host_device_map([3, 5, 6], [-1, -1, -1], [0, 1, 0, 1]) == [3, 5, 6, 3]
+    # a subset list (ELECT_EC_DEVICES=2,5): each socket's one GPU
+    assert _lib.host_device_map([2, 5], [0, 1], [1, 0, 1, 0]) == [5, 2, 5, 2]
+    # uneven sockets: 1 GPU on node 0, 3 on node 1
+    assert _lib.host_device_map([0, 1, 2, 3], [0, 1, 1, 1], [0, 1, 1, 1, 1, 0]) == [0, 1, 2, 3, 1, 0]
+    with pytest.raises(Exception):
+        _lib.host_device_map([], [], [0])

@@ -33,7 +33,7 @@ def _pinned(n, fill=None, keep=None):
 
 def _delta(before):
     now = _lib.host_path_stats()
-    return {k: now[k] - before[k] for k in now}
+    return {k: now[k] - before[k] for k in now if isinstance(now[k], (int, float))}
 
 
 @pytest.mark.parametrize("L", [4404020, 65536 + 3, 1 << 20, 1000])

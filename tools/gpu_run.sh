@@ -374,12 +374,12 @@ for step in "$@"; do
             ELECT_EC_DISPATCH_WAIT=$mode ELECT_EC_POLL_US=$us run "waitab_${w}_py_$i" 300 python bench.py --config hostpath \
                 --threads 64 --host-seconds 2 || exit $?
         done; done ;;
-    hostab)  # host path A/B (round 6): HOSTAB="name:VAR=v,VAR2=w;name2:..." x T_LIST x OPS, interleaved REPS times
+    hostab)  # host path A/B (round 6): HOSTAB="name:VAR=v,VAR2=w[:--arg,val];name2:..." x T_LIST x OPS, interleaved REPS times
         IFS=';' read -ra VARS <<< "${HOSTAB:-base:}"
         for i in $(seq 1 ${REPS:-1}); do for op in ${OPS:-encode}; do for T in ${T_LIST:-1 8 64}; do for v in "${VARS[@]}"; do
-            name=${v%%:*}; envs=${v#*:}
-            env ${envs//,/ } timeout -k 10 200 python bench.py --config hostpath --threads $T --host-op $op \
-                --host-seconds ${HOST_S:-2} --steps 8 --host-alloc ${ALLOC:-pageable} > "gpurun_out/hostab_${name}_${op}_T${T}_$i.log" 2>&1
+            name=${v%%:*}; rest=${v#*:}; envs=${rest%%:*}; bargs=""; [ "$rest" != "$envs" ] && bargs=${rest#*:}
+            env ELECT_AB=1 ${envs//,/ } timeout -k 10 200 python bench.py --config hostpath --threads $T --host-op $op \
+                --host-seconds ${HOST_S:-2} --steps 8 --host-alloc ${ALLOC:-pageable} ${bargs//,/ } > "gpurun_out/hostab_${name}_${op}_T${T}_$i.log" 2>&1
             rc=$?; echo "[$(date +%T)] hostab $name $op T$T rep $i rc=$rc" | tee -a gpurun_out/status.txt
             [ $rc -eq 0 ] || exit $rc
         done; done; done; done
