@@ -427,6 +427,20 @@ def cpu_baseline(args, k, m, L, stripes):
     reps, total_t, rate, place, threads = sweep[best]
     out = np.empty((stripes, 1, L), np.uint8)
     reps1, t1 = loop(base, out, 1, args.cpu_seconds * 0.3, 1)  # single-core figure
+    # one synchronous call as ELECT makes it, on one core: the degraded-read decode
+    # (ECRecovery.java:141; 4 survivors -> 1 unit) and the encode (4 -> 2) of one stripe
+    # of codeLength 4,404,020 B, the lone-caller GPU calls' counterpart (hostpath_lone)
+    Lc = 4404020
+    one = np.empty((1, n, Lc), np.uint8)
+    orc.fill_splitmix(0x10E, one)
+    one_out = np.empty((1, 1, Lc), np.uint8)
+    lone = {}
+    for name, coef, src, dst, buf_out, dst_stride in (
+            ("encode", enc_coef, [j * Lc for j in range(k)], [(k + r) * Lc for r in range(m)], one, n * Lc),
+            ("decode", dec_coef, [j * Lc for j in range(1, k + 1)], [0], one_out, Lc)):
+        ts = [orc.batch_apply(coef, one, n * Lc, src, buf_out, dst_stride, dst, Lc, 1, 1, level) for _ in range(15)]
+        lone[name] = round(sorted(ts)[7] * 1e3, 4)
+    assert np.array_equal(one_out[0, 0], one[0, 0]), "CPU baseline lone decode mismatch"
     return {
         "value": round(rate, 3),
         "unit": "GiB/s",
@@ -440,6 +454,8 @@ def cpu_baseline(args, k, m, L, stripes):
         # host path's cpu_core_ms_per_GiB, what offloading saves the node's cores
         "core_ms_per_GiB": round(1e3 * threads / rate, 2),
         "single_core_ms_per_GiB": round(1e3 * t1 / (reps1 * step_bytes / GIB), 2),
+        "one_call_1_core_ms": lone,  # median of 15, ELECT's codeLength
+        "one_call_workload": "one RS(6,4) call of 4 x 4,404,020 B on one core: encode (2 parity), decode (erase 0)",
         "working_set_bytes": int(base.nbytes + out.nbytes),
         "cpu_model": info["model"],
         "affinity_cpus": info["affinity"],
@@ -458,12 +474,24 @@ def host_inclusive(coder, k, m, L, stripes_total, dev, world=1):
     copy directions stay busy; 32 MiB of data per transfer
     (tools/tune/host_sweep.py staged: 47.8 GiB/s there, the PCIe ceiling for
     4 units in and 2 out is ~48 GiB/s)."""
+    from elect_amd import _lib
     from elect_amd.batch import encode_batch
     chunk = max(1, (32 << 20) // (k * L))  # stripes per transfer (32 MiB of data)
     nch = max(4, stripes_total // chunk)
     ring = 3
-    h_data = torch.randint(0, 256, (nch * chunk, k, L), dtype=torch.uint8).pin_memory()
-    h_par = torch.empty((nch * chunk, m, L), dtype=torch.uint8).pin_memory()
+    # the host buffers on the GPU's NUMA node (first touch while bound there; the
+    # affinity is restored after): a node-remote buffer costs up to 15 % of the
+    # link rate at low concurrency (profiles/r06/numa_ab.txt)
+    aff = os.sched_getaffinity(0)
+    nodes, gnode = numa_cpus(), _lib.device_numa_node(dev.index if dev.index is not None else 0)
+    if gnode in nodes:
+        os.sched_setaffinity(0, set(nodes[gnode]))
+    try:
+        h_data = torch.randint(0, 256, (nch * chunk, k, L), dtype=torch.uint8).pin_memory()
+        h_par = torch.empty((nch * chunk, m, L), dtype=torch.uint8).pin_memory()
+        h_par.fill_(0)
+    finally:
+        os.sched_setaffinity(0, aff)
     s_in, s_cmp, s_out = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
     dd = [torch.empty((chunk, k, L), dtype=torch.uint8, device=dev) for _ in range(ring)]
     dp = [torch.empty((chunk, m, L), dtype=torch.uint8, device=dev) for _ in range(ring)]
@@ -498,20 +526,26 @@ def host_inclusive(coder, k, m, L, stripes_total, dev, world=1):
         run()
         rates.append(nch * chunk * k * L / (time.perf_counter() - t0) / GIB)
     # every rank at once (each over its own PCIe link): 3 passes between barriers,
-    # aggregate = all ranks' data / the slowest rank's time
+    # aggregate = all ranks' data / the slowest rank's time; each pass's own rate is
+    # kept (round 5's driver line had the aggregate 15 % under the median)
     barrier(world)
     t0 = time.perf_counter()
+    marks = [t0]
     for _ in range(3):
         run()
-    own = time.perf_counter() - t0
+        marks.append(time.perf_counter())
+    own = marks[-1] - t0
     barrier(world)
     agg = world * 3 * nch * chunk * k * L / max_over_ranks(own, world) / GIB
+    passes = [round(nch * chunk * k * L / (b - a) / GIB, 2) for a, b in zip(marks, marks[1:])]
     ref = torch.empty((chunk, m, L), dtype=torch.uint8, device=dev)
     encode_batch(coder, h_data[-chunk:].to(dev), ref)
     torch.cuda.synchronize()
     if not torch.equal(ref.cpu(), h_par[-chunk:]):
         raise RuntimeError("host-inclusive pipeline: parity mismatch")
-    return round(sorted(rates)[2], 2), round(agg, 2)
+    detail = {"single_passes_GiB/s": [round(x, 2) for x in rates], "sum_passes_GiB/s": passes,
+              "host_numa_node": gnode if gnode in nodes else None}
+    return round(sorted(rates)[2], 2), round(agg, 2), detail
 
 
 def decode_sweep(coder, stripe, stream, reps=5):
@@ -907,8 +941,18 @@ def config_mixed(args, world, rank, dev):
             t["decode"].append(ev[1].elapsed_time(ev[2]))
         B, Lc = st.shape[0], st.shape[2]  # the coding view (tiled: B*L/64K stripes of 64 KiB)
         enc_ms, dec_ms = sorted(t["encode"])[4], sorted(t["decode"])[4]
+        # each launch's own access pattern with the GF work taken out (the same columns, strides
+        # and lengths: the unit-major [k+m][B][L] layout of the small classes, tiles for 1 MiB):
+        # frac_of_mix = probe time / kernel time
+        enc_mix = mix_ceiling([st[:, j] for j in range(k)], [st[:, k + r] for r in range(m)], Lc)
+        dec_mix = mix_ceiling([st[:, j] for j in (k, 1, 2, 3)], [out[:, 0]], Lc)
         per_class[f"{L}B"] = {"encode_frac": round(B * (k + m) * Lc / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                              "decode_frac": round(B * (k + 1) * Lc / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                              "decode_frac": round(B * (k + 1) * Lc / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "encode_mix_frac": round(B * (k + m) * Lc / (enc_mix["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "decode_mix_frac": round(B * (k + 1) * Lc / (dec_mix["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "encode_frac_of_mix": round(enc_mix["ms"] / enc_ms, 4),
+                              "decode_frac_of_mix": round(dec_mix["ms"] / dec_ms, 4),
+                              "mix_blocks": [enc_mix["block"], dec_mix["block"]]}
     if args.mixed_share:  # one GPU's share of an N-GPU run, timed alone: its own rate, and N x it
         per_gpu = args.steps * share_bytes / dt / GIB
         return {"metric": f"GiB/s device-resident RS(6,4) encode+decode, mixed chunks: one GPU's share of an "
@@ -1202,6 +1246,14 @@ def hostpath_child_cmd(ndev: int, alloc: str = "pageable") -> list:
             "--host-seconds", "2", "--host-alloc", alloc]
 
 
+def hostpath_lone_cmd(op: str) -> list:
+    """One caller on one device, ELECT's codeLength, pageable units, bound to the
+    device's NUMA node: ELECT's degraded read (one synchronous decodeImpl,
+    JEC/net/ECRecovery.java:141) or a lone encode, with per-call latency."""
+    return [sys.executable, os.path.abspath(__file__), "--config", "hostpath", "--threads", "1", "--host-chunk",
+            "4404020", "--batch", "1", "--host-op", op, "--host-seconds", "1", "--host-numa", "local"]
+
+
 def child_env() -> dict:
     """This environment without the launcher's rank variables: the child is a
     single process of its own (bench.py refuses a WORLD_SIZE that disagrees with
@@ -1226,7 +1278,9 @@ def hostpath_all_devices(args, world, rank, child=None):
     barrier(world)
     if rank == 0:
         ndev = world if child is not None else min(world, torch.cuda.device_count())
-        runs = [("pageable", child)] if child is not None else [("pageable", None), ("pinned", None)]
+        runs = [("pageable", child)] if child is not None else [("pageable", None), ("pinned", None),
+                                                                ("lone_decode", hostpath_lone_cmd("decode")),
+                                                                ("lone_encode", hostpath_lone_cmd("encode"))]
         deadline = time.monotonic() + HOSTPATH_TOTAL_TIMEOUT_S
         for alloc, cmd_override in runs:
             cmd = cmd_override if cmd_override is not None else hostpath_child_cmd(ndev, alloc)
@@ -1246,7 +1300,7 @@ def hostpath_all_devices(args, world, rank, child=None):
             else:
                 o = json.loads(line)
                 rec = {"value": o["value"], "unit": o["unit"], "devices": o["devices"], "callers": o["callers"],
-                       "host_alloc": o.get("host_alloc"),
+                       "host_alloc": o.get("host_alloc"), "call_latency_ms": o.get("call_latency_ms"),
                        "cpu_core_ms_per_GiB": o.get("cpu_core_ms_per_GiB"),
                        "cpu_bound_ceiling_GiB/s": o.get("cpu_bound_ceiling_GiB/s"),
                        "cpu_quota_cores": o.get("cpu_quota_cores"),
@@ -1867,10 +1921,11 @@ def main():
                                                                                   "decode_shape")}
         rf["torch_copy_GB/s"] = device_copy_rate(dev)
     if not args.no_host:  # every rank, over its own PCIe link, at the same time
-        own_rate, agg = host_inclusive(coder, k, m, L, min(B, 4096), dev, world)
+        own_rate, agg, hi_detail = host_inclusive(coder, k, m, L, min(B, 4096), dev, world)
         rates = gather(own_rate, world)
         out["host_inclusive_GiB/s"] = rates[0]
         out["host_inclusive_sum_GiB/s"] = agg
+        out["host_inclusive_passes"] = hi_detail
         out["host_inclusive_per_rank_GiB/s"] = rates
     if not args.no_host and not args.no_hostpath:  # ELECT's own calls over all the job's devices
         hp = hostpath_all_devices(args, world, rank)
@@ -1882,6 +1937,19 @@ def main():
             rec["verified"] = rec["verified"] and hp["verified"]
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args, k, m, L, B)
+    hp = out.get("hostpath_all_devices") or {}
+    lone = {}
+    for op in ("decode", "encode"):  # a lone caller's synchronous call (ECRecovery.java:141) against one CPU core
+        r = hp.get(f"lone_{op}")
+        if isinstance(r, dict) and r.get("value") is not None:
+            lat = r.get("call_latency_ms") or {}
+            lone[op] = {"GiB/s": r["value"], "p50_ms": lat.get("p50"), "p99_ms": lat.get("p99"),
+                        "mean_ms": lat.get("mean")}
+            cb = out.get("cpu_baseline") or {}
+            if (cb.get("one_call_1_core_ms") or {}).get(op):
+                lone[op]["oracle_1_core_ms"] = cb["one_call_1_core_ms"][op]
+    if lone:
+        out["hostpath_lone_caller"] = lone
     finish(out, rank, world, rec)
 
 

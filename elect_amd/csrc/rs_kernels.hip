@@ -14,8 +14,10 @@ namespace {
 // Hash-partial scratch when the caller brings none (the device-resident API):
 // one buffer per (device, stream), reused only in that stream's order.  It is
 // handed to another stream (64 entries per device, least recently used first)
-// only after a device-wide synchronize, and grown only after its own stream's
-// synchronize, so a hashed call records nothing on the stream: a completion
+// only after its last use (an event recorded behind each use once 32 or more
+// entries are assigned; a device-wide synchronize before that, round 6), and
+// grown only after its own stream's synchronize, so a hashed call records
+// nothing on the stream while few streams share the cache: a completion
 // marker behind every call held the next launch back ~1.5 us (round 4,
 // profiles/r04/event_cost.txt), and streams beyond 64 are rare (16 entries made
 // the device-wide synchronize of a handoff routine for 17+ concurrently launching streams).
@@ -32,7 +34,14 @@ struct ScratchEntry {
     size_t words = 0;
     hipStream_t owner = nullptr;  // the stream whose launches may still read ptr
     bool owned = false;
+    // Under pressure (kPressure or more entries assigned) each release records `ev` on
+    // its stream, so that a handoff waits for that stream's last use only
+    // (hipStreamWaitEvent) instead of the whole device.
+    bool record = false;    // this lease records on release
+    hipEvent_t ev = nullptr;
+    bool ev_valid = false;  // ev marks the last use (else: device-wide synchronize at handoff)
 };
+constexpr int kPressure = 32;
 
 struct ScratchCache {
     std::mutex mu;
@@ -60,10 +69,14 @@ hipError_t scratch_lease(hipStream_t stream, size_t words, ScratchEntry** out)
     ScratchCache& c = g_scratch[dev];
     for (;;) {
         ScratchEntry* e = nullptr;
+        bool pressure = false;
         {
             std::lock_guard<std::mutex> lock(c.mu);
-            for (ScratchEntry& x : c.e)
+            int assigned = 0;
+            for (ScratchEntry& x : c.e) {
+                assigned += x.assigned;
                 if (x.assigned && x.stream == stream) e = &x;
+            }
             if (!e) {  // a free entry, else the least recently used one
                 for (ScratchEntry& x : c.e)
                     if (!e || (!x.assigned && e->assigned) || (x.assigned == e->assigned && x.last < e->last)) e = &x;
@@ -71,15 +84,24 @@ hipError_t scratch_lease(hipStream_t stream, size_t words, ScratchEntry** out)
                 e->stream = stream;
             }
             e->last = ++c.tick;
+            // (ELECT_EC_SCRATCH_EVENTS=0: never record, round 5's device-wide synchronize at every handoff; A/B)
+            static const bool events = [] {
+                const char* v = std::getenv("ELECT_EC_SCRATCH_EVENTS");
+                return !(v && std::atoi(v) == 0);
+            }();
+            pressure = events && assigned >= kPressure;
         }
         e->mu.lock();
         if (!e->assigned || e->stream != stream) {  // taken over for another stream meanwhile
             e->mu.unlock();
             continue;
         }
-        // Last used on another stream (which may since have been destroyed): wait for
-        // the whole device, then this stream owns the buffer.
-        if (e->owned && e->owner != stream) err = hipDeviceSynchronize();
+        // Last used on another stream (which may since have been destroyed): wait for its
+        // last use (the event recorded then, device-side), else for the whole device;
+        // then this stream owns the buffer.
+        if (e->owned && e->owner != stream)
+            err = e->ev_valid ? hipStreamWaitEvent(stream, e->ev, 0) : hipDeviceSynchronize();
+        e->record = pressure;
         if (err == hipSuccess && e->words < words) {
             if (e->owned) err = hipStreamSynchronize(stream);  // its last use, on this stream
             if (err == hipSuccess && e->ptr) err = hipFree(e->ptr);
@@ -99,10 +121,17 @@ hipError_t scratch_lease(hipStream_t stream, size_t words, ScratchEntry** out)
     }
 }
 
-hipError_t scratch_release(ScratchEntry* e, hipStream_t)
+hipError_t scratch_release(ScratchEntry* e, hipStream_t stream)
 {
+    hipError_t err = hipSuccess;
+    e->ev_valid = false;
+    if (e->record) {  // (a marker behind every call would hold the next launch back ~1.5 us: only under pressure)
+        if (!e->ev) err = hipEventCreateWithFlags(&e->ev, hipEventDisableTiming);
+        if (err == hipSuccess) err = hipEventRecord(e->ev, stream);
+        e->ev_valid = err == hipSuccess;
+    }
     e->mu.unlock();
-    return hipSuccess;
+    return err;
 }
 
 // Every (cols, rows) launcher, by source-column count (rs_inst.hip).  Padded

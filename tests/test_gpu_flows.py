@@ -432,3 +432,73 @@ def test_concurrent_streams_hashed_device_api(dev, oracle, threads):
     for x in th:
         x.join()
     assert not errors, errors[:5]
+
+
+def test_scratch_handoff_waits_for_last_use_only(dev, oracle):
+    """More streams than the hash scratch cache holds (64 per device): once 32 or
+    more entries are assigned, each use records an event, and a handoff to
+    another stream waits for that event on the device (hipStreamWaitEvent)
+    instead of synchronizing the device from the calling thread
+    (rs_kernels.hip scratch_lease).  80 streams launch hashed
+    batches while an unrelated stream reads HBM for ~0.3 s: a device-wide
+    synchronize at a handoff would hold the launching call until that work is
+    done, so every launch of the last round must return in far less time (the
+    launches' completion is not timed: with 4 hardware queues per process,
+    streams share queues with the long work), and the hashes stay right."""
+    import threading
+    import time
+    from elect_amd import _lib
+    from elect_amd.batch import encode_batch_ex
+    from elect_amd.coder import RSCoder
+    k, m, B, L, S = 4, 2, 2, 65536 + 4, 80
+    coder, enc = RSCoder(k, m), oracle.Encoder(k, m)
+    rng = np.random.default_rng(99)
+    data = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    d = torch.from_numpy(data).to(dev)
+    want = [enc.encode([data[b, j] for j in range(k)]) for b in range(B)]
+    streams = [torch.cuda.Stream(dev) for _ in range(S)]
+    outs = [(torch.empty((B, m, L), dtype=torch.uint8, device=dev), torch.empty((B, m), dtype=torch.int32, device=dev))
+            for _ in range(S)]
+    errors, launch_s = [], [0.0] * S
+
+    def round_of_calls():
+        def one(i):
+            try:
+                torch.cuda.set_device(dev)
+                par, hs = outs[i]
+                t0 = time.perf_counter()
+                encode_batch_ex(coder, d, par, hashes=hs, stream=streams[i])
+                launch_s[i] = time.perf_counter() - t0
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+        th = [threading.Thread(target=one, args=(i,)) for i in range(S)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+
+    round_of_calls()
+    torch.cuda.synchronize()
+    round_of_calls()  # every entry's last use now recorded under pressure
+    torch.cuda.synchronize()
+    buf = torch.empty(1 << 31, dtype=torch.uint8, device=dev)
+    sink = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    long_stream = torch.cuda.Stream(dev)
+    t0 = time.perf_counter()
+    for _ in range(1000):  # 1,000 x 2 GiB reads: ~0.3 s on an MI355X
+        _lib.hbm_probe(0, buf.data_ptr(), sink.data_ptr(), buf.numel(), stream=long_stream.cuda_stream)
+    round_of_calls()
+    slowest_launch = max(launch_s)
+    long_stream.synchronize()
+    long_s = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    assert not errors, errors[:3]
+    for par, hs in outs:
+        got_p, got_h = par.cpu().numpy(), hs.cpu().numpy()
+        for b in range(B):
+            for r in range(m):
+                assert np.array_equal(got_p[b, r], want[b][r])
+                assert int(got_h[b, r]) == oracle.java_hashcode(want[b][r])
+    assert long_s > 0.15, f"the unrelated work ran only {long_s:.3f} s: no room for the timing check"
+    assert slowest_launch < long_s / 3, (f"a hashed launch took {slowest_launch * 1e3:.1f} ms beside {long_s * 1e3:.0f} ms "
+                                         "of unrelated work: a scratch handoff synchronized the device")

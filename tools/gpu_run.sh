@@ -1,7 +1,8 @@
 #!/bin/bash
 # GPU-box runner: each GPU step under its own time limit; stop on any fault,
 # abort, segfault, timeout or hang (exit codes other than 0 / pytest's 1).
-# usage: tools/gpu_run.sh step [step ...]   steps: smoke tests bench prof pmc tune
+# usage: tools/gpu_run.sh step [step ...]   steps: smoke tests bench prof pmc tune ...
+# (round 6: steps that A/B'd knobs the library no longer reads were removed; their results stay in profiles/)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -133,21 +134,11 @@ for step in "$@"; do
             ELECT_EC_REGISTER_SLOTS=$sl run "bench_hostpath_reg${rg}_s${sl}_T${T}_$i" 300 python bench.py --config hostpath \
                 --threads $T --host-register $rg --host-seconds 2 --steps 8 --host-op ${HOST_OP:-encode} || exit $?
         done; done; done; done ;;
-    hostpinned)  # page-locked pool callers: gather/scatter kernels vs round 4's per-unit DMAs, interleaved
-        for i in 1 2; do for mv in kernel dma; do for T in ${T_LIST:-64 16}; do
-            ELECT_EC_DIRECT_MOVE=$mv run "bench_hostpath_pinned_${mv}_T${T}_$i" 300 python bench.py --config hostpath \
-                --threads $T --host-alloc pinned --host-seconds 2 --steps 8 --host-op ${HOST_OP:-encode} || exit $?
-        done; done; done ;;
     hostcopyvar)  # the direct batches' gather/scatter kernel variants (ELECT_EC_COPY_VARIANT), pinned and pageable
         for i in 1 2; do for v in ${VARIANTS:-0 1 2 3}; do for cb in ${COPY_BLOCKS:-512}; do for alloc in ${ALLOCS:-pinned pageable}; do
             ELECT_EC_COPY_VARIANT=$v ELECT_EC_COPY_BLOCKS=$cb run "bench_hostpath_cv${v}_cb${cb}_${alloc}_T64_$i" 300 python bench.py --config hostpath \
                 --threads 64 --host-alloc $alloc --host-seconds 2 --steps 8 || exit $?
         done; done; done; done ;;
-    hostblock)  # the dispatcher's wait on the previous batch: polled (default) vs blocking event, interleaved
-        for i in 1 2; do for b in 0 1; do for alloc in ${ALLOCS:-pageable pinned}; do
-            ELECT_EC_DISPATCH_BLOCKING=$b run "bench_hostpath_blk${b}_${alloc}_T64_$i" 300 python bench.py --config hostpath \
-                --threads 64 --host-alloc $alloc --host-seconds 2 --steps 8 || exit $?
-        done; done; done ;;
     cauchycap)  # RS(12,8) encode vs the occupancy cap (ELECT_EC_WRITE_WAVES), both forms, interleaved
         for i in 1 2; do for w in ${CAPS:-12 16 20 24}; do for c in 1 0; do
             ELECT_EC_WRITE_WAVES=$w ELECT_EC_CAUCHY=$c run "bench_rs12_cap${w}_cauchy${c}_$i" 300 python bench.py --config rs12 --steps 50 || exit $?
@@ -242,16 +233,6 @@ for step in "$@"; do
                     -- python3 bench.py --config padded --pad-fill $fill --steps 20 || exit $?
             done
         done ;;
-    persist)  # persistent plain/grouped kernels (build first: tools/ab_build.sh persist -DAB_PERSIST=1; ELECT_EC_LIB=elect_amd/_ab/libelect_ec_persist.so ELECT_EC_PERSIST=1): GPU suite under it, then interleaved A/B
-        export ELECT_EC_LIB=$PWD/elect_amd/_ab/libelect_ec_persist.so
-        ELECT_EC_PERSIST=1 run pytest_gpu_persist 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 || exit $?
-        for i in 1 2 3; do for P in 0 1; do
-            ELECT_EC_PERSIST=$P run "persist${P}_headline_$i" 300 python bench.py --no-cpu --no-host --no-configs --steps 50 || exit $?
-            ELECT_EC_PERSIST=$P run "persist${P}_mixed8_$i" 300 python bench.py --config mixed --mixed-share 8 --steps 50 || exit $?
-            ELECT_EC_PERSIST=$P run "persist${P}_mixed_$i" 300 python bench.py --config mixed --steps 50 || exit $?
-            ELECT_EC_PERSIST=$P run "persist${P}_rs12_$i" 300 python bench.py --config rs12 --steps 50 || exit $?
-        done; done
-        unset ELECT_EC_LIB ;;
     zerocopy) run zerocopy 600 python tools/tune/zerocopy_probe.py || exit $? ;;
     zchost)  # the product's host path with zero-copy lone callers: tests, then callers 1 / 2 / 16 / 64, on vs off
         run pytest_zerocopy 600 python -m pytest tests/test_gpu_zerocopy.py -x -q -p no:cacheprovider --timeout 300 || exit $?
@@ -286,23 +267,6 @@ for step in "$@"; do
                     -d $OUT/sqpmc_${cfg}_$pass -o run -- python3 bench.py $args || exit $?
             done
         done ;;
-    hostwait)  # host-path waits: blocking events + completion thread / polling events / round 3's callbacks (round 4;
-               # the recipe of profiles/r04/hostwait_ab.txt: ELECT_EC_HOST_WAIT was removed with the losing modes)
-        for i in 1 2; do for w in ${WAIT_MODES:-block spin callback}; do for T in ${WAIT_T:-1 16 64}; do
-            ELECT_EC_HOST_WAIT=$w run "hostwait_${w}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
-                --host-op ${HOST_OP:-encode} --host-seconds ${HOST_S:-2} || exit $?
-        done; done; done ;;
-    hostdirect)  # page-locked caller buffers (elect_ec_host_alloc, direct batches) vs pageable, x waits (round 4)
-        for i in 1 2; do for al in ${ALLOCS:-pinned pageable}; do for w in ${WAIT_MODES:-callback block}; do for T in ${WAIT_T:-1 16 64}; do
-            ELECT_EC_HOST_WAIT=$w run "hostdirect_${al}_${w}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
-                --host-op ${HOST_OP:-encode} --host-seconds ${HOST_S:-2} --host-alloc $al || exit $?
-        done; done; done; done ;;
-    directstreams)  # direct batches: per-unit DMAs on 1 or 2 streams (round 4; the recipe of direct_streams_ab.txt:
-                    # ELECT_EC_DIRECT_STREAMS was removed with the 2-stream variant)
-        for i in 1 2; do for ds in 2 1; do for T in ${WAIT_T:-64 16 1}; do
-            ELECT_EC_DIRECT_STREAMS=$ds run "directstreams_s${ds}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
-                --host-seconds ${HOST_S:-2} --host-alloc pinned || exit $?
-        done; done; done ;;
     ldsprobe)  # HBM streams loaded through LDS (global_load_lds_dwordx4) vs into VGPRs (round 4; build tools/tune/lds_probe first)
         run ldsprobe 300 tools/tune/lds_probe || exit $? ;;
     pinzc)  # a lone caller on pool buffers: zero-copy in place (default) vs direct batches (round 4)
@@ -310,12 +274,6 @@ for step in "$@"; do
             ELECT_EC_ZEROCOPY=$z run "pinzc_z${z}_$i" 300 python bench.py --config hostpath --threads 1 \
                 --host-seconds ${HOST_S:-2} --host-alloc pinned || exit $?
         done; done ;;
-    copyisa)  # pageable staging copies: AVX-512 vs SSE2 streaming stores (round 4; the recipe of copy_isa_ab.txt:
-              # ELECT_EC_COPY_ISA was removed with the AVX-512 copies)
-        for i in 1 2; do for isa in avx512 sse; do for T in ${WAIT_T:-64 16 1}; do
-            ELECT_EC_COPY_ISA=$isa run "copyisa_${isa}_T${T}_$i" 300 python bench.py --config hostpath --threads $T \
-                --host-seconds ${HOST_S:-2} || exit $?
-        done; done; done ;;
     final)  # the round's judged artefacts: GPU suite, smoke, the driver's bench command, rocprof stats, PMC traffic,
             # the BASELINE configs and the fused steps (collect with tools/collect_final.sh)
         run pytest_gpu 1000 python -m pytest tests -m gpu -x -q -p no:cacheprovider
@@ -364,16 +322,6 @@ for step in "$@"; do
         for m in ${SPIN_MODES:-idle kernels hostfunc hostfunc_burst event blocking hsa_lock longk_hostfunc longk_sync}; do
             run "spin_$m" 60 tools/tune/spin_probe $m || exit $?
         done ;;
-    waitab)  # batch completion: poller thread (default, ELECT_EC_POLL_US 25 / 50) vs host-function callbacks, interleaved;
-             # C++ callers with per-thread CPU, then the Python bench, pageable and pool units
-        for i in 1 2; do for w in poll25 poll50 callback; do
-            mode=${w%%[0-9]*}; us=${w#poll}; [ "$mode" = poll ] || us=25
-            for pool in 0 1; do
-                ELECT_EC_DISPATCH_WAIT=$mode ELECT_EC_POLL_US=$us run "waitab_${w}_c${pool}_$i" 120 tools/hostpath_cbench 64 3 4404020 4 $pool || exit $?
-            done
-            ELECT_EC_DISPATCH_WAIT=$mode ELECT_EC_POLL_US=$us run "waitab_${w}_py_$i" 300 python bench.py --config hostpath \
-                --threads 64 --host-seconds 2 || exit $?
-        done; done ;;
     hostab)  # host path A/B (round 6): HOSTAB="name:VAR=v,VAR2=w[:--arg,val];name2:..." x T_LIST x OPS, interleaved REPS times
         IFS=';' read -ra VARS <<< "${HOSTAB:-base:}"
         for i in $(seq 1 ${REPS:-1}); do for op in ${OPS:-encode}; do for T in ${T_LIST:-1 8 64}; do for v in "${VARS[@]}"; do
@@ -398,16 +346,6 @@ for step in "$@"; do
     piecekb)  # gather / scatter piece size (ELECT_EC_PIECE_KB) at 8 and 64 callers, interleaved, 3 s runs
         for i in ${PIECE_RUNS:-1 2}; do for kb in ${PIECE_KBS:-64 32 16 8}; do for T in ${T_LIST:-8 64}; do
             ELECT_EC_PIECE_KB=$kb run "piecekb_${kb}_T${T}_$i" 300 python bench.py --config hostpath --threads $T --host-seconds 3 || exit $?
-        done; done; done ;;
-    zcwaves)  # a lone caller: zero-copy launches capped at W waves per CU (ELECT_EC_ZC_WAVES) vs the batched path
-        for i in 1 2; do for w in ${ZC_WAVES:-off 0 1 2 4 8}; do
-            if [ $w = off ]; then z=0; else z=1; fi
-            ELECT_EC_ZEROCOPY=$z ELECT_EC_ZC_WAVES=${w/off/0} run "zcwaves_${w}_T${T:-1}_$i" 300 python bench.py --config hostpath \
-                --threads ${T:-1} --host-seconds 2 || exit $?
-        done; done ;;
-    gateab)  # dispatch gate (a batch waits for the previous batch's inputs to land) on / off, C++ callers, interleaved
-        for i in 1 2; do for g in 1 0; do for T in ${T_LIST:-8 16 64}; do
-            ELECT_EC_DISPATCH_GATE=$g run "gateab_g${g}_T${T}_$i" 120 tools/hostpath_cbench $T 3 4404020 4 0 || exit $?
         done; done; done ;;
     bitslice)  # RS(12,8) encode: bitsliced (tools/tune/bitslice_probe.hip, built here) vs the product, bytes compared,
                # then SQ counters of both kernels in one pass (VALU instructions, waves, GUI-active cycles for the clock)

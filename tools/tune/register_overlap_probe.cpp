@@ -17,7 +17,11 @@
 // call, interior moved by DMA, the <= 2 ragged edge pages by pageable copies,
 // then unregistered).  Prints calls/s, data GiB/s, core-ms per GiB.
 //
-//   hipcc -O2 -std=c++17 tools/tune/register_overlap_probe.cpp -lpthread -o tools/tune/register_overlap_probe
+// Part 5 (relock, round 6): see relock() below.
+//
+//   hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/tune/register_overlap_probe.cpp -L/opt/rocm/lib
+//       -lhsa-runtime64 -lpthread -o tools/tune/register_overlap_probe
+//   tools/tune/register_overlap_probe [all | S1..S8 | D1 | cost | unregwait | hsalock | relock]
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -488,6 +492,125 @@ static void hsalock()
     for (auto* x : bufs) std::free(x);
 }
 
+
+// Part 5 (round 6): do stale GPU mappings survive
+// hsa_amd_memory_unlock?  The round-5 zero-copy fault (ECDeviceError in
+// test_lone_caller_copy_fanout) was put down to "the HSA runtime keeps unlocked
+// ranges cached"; this checks the mechanism.  On an anonymous mapping: lock
+// pages [4, 36), read (kernel), write (kernel) and DMA-read (SDMA,
+// hsa_amd_memory_async_copy) through the returned address, unlock; then the
+// mapping's pages are REPLACED (munmap + mmap MAP_FIXED: new physical pages at
+// the same virtual addresses, as a free + malloc can do) and refilled with a new
+// pattern; then overlapping, shifted [10, 50) is locked and read / written /
+// DMA'd again, and so is the identical [4, 36), and hipHostRegister of
+// [8, 40) (round 5's two-layer sequence).  A stale cached translation would
+// show the old pattern (or a fault) on the device side.
+__global__ void fill_kernel(uint4* dst, size_t n16, uint32_t v)
+{
+    for (size_t i = blockIdx.x * size_t{blockDim.x} + threadIdx.x; i < n16; i += size_t{gridDim.x} * blockDim.x)
+        dst[i] = make_uint4(v, v, v, v);
+}
+
+static void relock()
+{
+    std::printf("\n# part 5: lock, unlock, replace the pages, relock overlapping / shifted / identical\n");
+    if (hsa_init() != HSA_STATUS_SUCCESS) {
+        std::printf("hsa_init failed\n");
+        return;
+    }
+    hsa_agent_t gpu{}, cpu{};
+    hsa_iterate_agents(find_gpu, &gpu);
+    hsa_iterate_agents(
+        [](hsa_agent_t a, void* out) -> hsa_status_t {
+            hsa_device_type_t t;
+            hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
+            if (t == HSA_DEVICE_TYPE_CPU) {
+                *static_cast<hsa_agent_t*>(out) = a;
+                return HSA_STATUS_INFO_BREAK;
+            }
+            return HSA_STATUS_SUCCESS;
+        },
+        &cpu);
+    const size_t pages = 64, bytes = pages * P;
+    auto* map = static_cast<uint8_t*>(mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0));
+    uint8_t* dev = nullptr;
+    (void)hipMalloc(reinterpret_cast<void**>(&dev), bytes);
+    hipStream_t s;
+    (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    hsa_signal_t sig{};
+    hsa_signal_create(1, 0, nullptr, &sig);
+    std::vector<uint8_t> back(bytes);
+    auto fill_host = [&](uint8_t v) {
+        for (size_t i = 0; i < bytes; ++i) map[i] = static_cast<uint8_t>(v + i / P);
+    };
+    // the device's view of [lo, hi) pages through address ap: kernel read, then SDMA read, each checked against host
+    auto check_view = [&](const char* tag, void* ap, size_t lo, size_t hi, uint8_t v) {
+        const size_t n = (hi - lo) * P;
+        (void)hipMemsetAsync(dev, 0, n, s);
+        pcie_copy<<<256, 256, 0, s>>>(static_cast<const uint4*>(ap), reinterpret_cast<uint4*>(dev), n / 16);
+        hipError_t e = hipMemcpyAsync(back.data(), dev, n, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        size_t bad_k = 0;
+        for (size_t i = 0; i < n; ++i) bad_k += back[i] != static_cast<uint8_t>(v + (lo * P + i) / P);
+        (void)hipMemset(dev, 0, n);
+        hsa_signal_store_screlease(sig, 1);
+        const hsa_status_t hs = hsa_amd_memory_async_copy(dev, gpu, ap, cpu, n, 0, nullptr, sig);
+        if (hs == HSA_STATUS_SUCCESS)
+            hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+        (void)hipMemcpy(back.data(), dev, n, hipMemcpyDeviceToHost);
+        size_t bad_d = 0;
+        for (size_t i = 0; i < n; ++i) bad_d += back[i] != static_cast<uint8_t>(v + (lo * P + i) / P);
+        // kernel write through the mapping, seen by the CPU at the host address
+        fill_kernel<<<64, 256, 0, s>>>(static_cast<uint4*>(ap), P / 16, 0xA5A5A5A5u);
+        const hipError_t ew = hipStreamSynchronize(s);
+        const bool w_ok = ew == hipSuccess && map[lo * P] == 0xA5 && map[lo * P + P - 1] == 0xA5;
+        for (size_t i = lo * P; i < lo * P + P; ++i) map[i] = static_cast<uint8_t>(v + i / P);  // restore
+        std::printf("%-44s agent ptr %s host: kernel read %s (%zu bad), DMA read %s (%zu bad, status %d), "
+                    "kernel write %s (rc %d/%d)\n",
+                    tag, ap == map + lo * P ? "==" : "!=", bad_k ? "STALE" : "ok", bad_k, bad_d ? "STALE" : "ok", bad_d,
+                    static_cast<int>(hs), w_ok ? "seen" : "NOT SEEN", static_cast<int>(e), static_cast<int>(ew));
+    };
+    auto lock = [&](size_t lo, size_t hi, void** ap) {
+        return hsa_amd_memory_lock(map + lo * P, (hi - lo) * P, &gpu, 1, ap);
+    };
+    fill_host(10);
+    void* ap = nullptr;
+    hsa_status_t st = lock(4, 36, &ap);
+    std::printf("lock [4, 36): status %d\n", static_cast<int>(st));
+    if (st == HSA_STATUS_SUCCESS) check_view("[4, 36) locked", ap, 4, 36, 10);
+    std::printf("unlock [4, 36): status %d\n", static_cast<int>(hsa_amd_memory_unlock(map + 4 * P)));
+    // new physical pages at the same virtual addresses
+    munmap(map, bytes);
+    auto* again = static_cast<uint8_t*>(mmap(map, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED, -1, 0));
+    std::printf("remapped at the same address: %s\n", again == map ? "yes" : "NO");
+    fill_host(100);
+    st = lock(10, 50, &ap);
+    std::printf("lock [10, 50) after the remap (overlapping, shifted): status %d\n", static_cast<int>(st));
+    if (st == HSA_STATUS_SUCCESS) {
+        check_view("[10, 50) relocked, shifted", ap, 10, 50, 100);
+        std::printf("unlock [10, 50): status %d\n", static_cast<int>(hsa_amd_memory_unlock(map + 10 * P)));
+    }
+    st = lock(4, 36, &ap);
+    std::printf("lock [4, 36) again (identical extent): status %d\n", static_cast<int>(st));
+    if (st == HSA_STATUS_SUCCESS) {
+        check_view("[4, 36) relocked, identical", ap, 4, 36, 100);
+        std::printf("unlock [4, 36): status %d\n", static_cast<int>(hsa_amd_memory_unlock(map + 4 * P)));
+    }
+    // round 5's two-layer sequence: an HSA lock and unlock, then hipHostRegister of an overlapping range
+    hipError_t he = hipHostRegister(map + 8 * P, 32 * P, hipHostRegisterMapped);
+    void* hp = nullptr;
+    if (he == hipSuccess) he = hipHostGetDevicePointer(&hp, map + 8 * P, 0);
+    std::printf("hipHostRegister [8, 40) after the HSA unlock: rc %d\n", static_cast<int>(he));
+    if (he == hipSuccess) {
+        check_view("[8, 40) hipHostRegister'ed", hp, 8, 40, 100);
+        std::printf("hipHostUnregister: rc %d\n", static_cast<int>(hipHostUnregister(map + 8 * P)));
+    }
+    (void)hipGetLastError();
+    hsa_signal_destroy(sig);
+    (void)hipFree(dev);
+    munmap(map, bytes);
+}
+
 int main(int argc, char** argv)
 {
     int ndev = 0;
@@ -501,6 +624,10 @@ int main(int argc, char** argv)
     (void)hipFree(nullptr);
     if (what == "hsalock") {
         hsalock();
+        return 0;
+    }
+    if (what == "relock") {
+        relock();
         return 0;
     }
     if (what == "unregwait") {
