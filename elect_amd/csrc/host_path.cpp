@@ -104,14 +104,18 @@ public:
     void* alloc(size_t bytes)
     {
         const size_t cls = std::max<size_t>(kClass, (bytes + kClass - 1) / kClass * kClass);
+        // Free blocks are kept per NUMA node: a block's pages were faulted in (locked) by the
+        // thread that made it, on that thread's node, and go back to a thread on the same
+        // node (the one the NUMA-aware device choice gives a GPU on).
+        const int node = current_node();
         {
             std::unique_lock<std::shared_mutex> lock(mu_);
-            auto it = free_.find(cls);
+            auto it = free_.find(Key{node, cls});
             if (it != free_.end() && !it->second.empty()) {
                 void* p = it->second.back();
                 it->second.pop_back();
                 free_bytes_ -= cls;
-                live_[reinterpret_cast<uintptr_t>(p)] = Block{cls, true, delta_[p]};
+                live_[reinterpret_cast<uintptr_t>(p)] = Block{cls, true, delta_[p], node};
                 return p;
             }
         }
@@ -146,7 +150,7 @@ public:
         }
         try {
             std::unique_lock<std::shared_mutex> lock(mu_);
-            live_[reinterpret_cast<uintptr_t>(p)] = Block{cls, pinned, delta};
+            live_[reinterpret_cast<uintptr_t>(p)] = Block{cls, pinned, delta, node};
             if (pinned) delta_[p] = delta;
         } catch (...) {  // no record, no buffer: nothing leaks
             release_block(p, pinned);
@@ -196,7 +200,7 @@ public:
             live_.erase(it);
             if (b.pinned && free_bytes_ + b.size <= cap()) {
                 try {
-                    free_[b.size].push_back(p);
+                    free_[Key{b.node, b.size}].push_back(p);
                     free_bytes_ += b.size;
                     return true;
                 } catch (...) {  // no room in the free list: release the buffer below
@@ -242,7 +246,18 @@ private:
         size_t size = 0;
         bool pinned = false;
         intptr_t delta = 0;  // device address - host address
+        int node = -1;       // NUMA node of the thread that made it (its pages were faulted in there)
     };
+    struct Key {
+        int node;
+        size_t cls;
+        bool operator<(const Key& o) const { return node != o.node ? node < o.node : cls < o.cls; }
+    };
+    static int current_node()
+    {
+        unsigned cpu = 0, node = 0;
+        return getcpu(&cpu, &node) == 0 ? static_cast<int>(node) : -1;
+    }
 
     // free page-locked bytes kept for reuse (ELECT_EC_HOST_POOL_MB, default 4096)
     static size_t cap()
@@ -256,7 +271,7 @@ private:
 
     mutable std::shared_mutex mu_;
     std::map<uintptr_t, Block> live_;
-    std::map<size_t, std::vector<void*>> free_;
+    std::map<Key, std::vector<void*>> free_;  // by (node, size class)
     std::map<void*, intptr_t> delta_;  // every page-locked block ever made (blocks are only ever reused)
     size_t free_bytes_ = 0;
 };

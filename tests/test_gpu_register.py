@@ -185,3 +185,65 @@ def test_partially_overlapping_units_of_concurrent_callers():
     st = json.loads(r.stdout.strip().split(" ", 1)[1])
     assert st["unregister_failures"] == 0 and st["per_thread"] == 0, st
     assert st["registered"] + st["batched"] == 24 and st["registered"] >= 1, st
+
+
+REMAP = r"""
+import ctypes, json, sys
+import numpy as np
+import torch
+sys.path.insert(0, ROOT)
+from elect_amd import _lib
+from elect_amd.coder import RSCoder
+from oracle import ec_oracle as orc
+
+torch.cuda.init()
+libc = ctypes.CDLL("libc.so.6", use_errno=True)
+libc.mmap.restype = ctypes.c_void_p
+libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+PROT_RW, MAP_PRIVATE, MAP_ANON, MAP_FIXED = 3, 0x02, 0x20, 0x10
+k, m, L = 4, 2, (1 << 20) + 4099
+size = (k + m + 1) * (L + 8192) + (1 << 20)
+base = libc.mmap(None, size, PROT_RW, MAP_PRIVATE | MAP_ANON, -1, 0)
+c, enc = RSCoder(k, m), orc.Encoder(k, m)
+bad = []
+for rnd in range(6):
+    if rnd:  # new physical pages at the same virtual addresses (a free + malloc can do this)
+        libc.munmap(base, size)
+        got = libc.mmap(base, size, PROT_RW, MAP_PRIVATE | MAP_ANON | MAP_FIXED, -1, 0)
+        assert got == base
+    buf = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(base))
+    shift = 1 + 1237 * rnd  # each round's units at another extent: locks overlap the last round's, shifted
+    rng = np.random.default_rng(rnd)
+    units = [buf[shift + i * (L + 8192):][:L] for i in range(k + m + 1)]
+    for x in units[:k]:
+        x[:] = rng.integers(0, 256, L, dtype=np.uint8)
+    a = lambda xs: [x.ctypes.data for x in xs]
+    c.encode_host(a(units[:k]), a(units[k:k + m]), L)
+    want = enc.encode([x.copy() for x in units[:k]])
+    if not all(np.array_equal(x, y) for x, y in zip(units[k:k + m], want)):
+        bad.append(f"round {rnd} encode")
+    c.decode_host(a([units[k]] + units[1:k]), [k, 1, 2, 3], [0], a([units[k + m]]), L)
+    if not np.array_equal(units[k + m], units[0]):
+        bad.append(f"round {rnd} decode")
+    del buf, units, x
+libc.munmap(base, size)
+print("BAD " + "; ".join(bad) if bad else "OK", json.dumps(_lib.host_path_stats()))
+"""
+
+
+def test_relocks_after_the_pages_were_replaced():
+    """The pattern the relock probe found unsafe for DMA (profiles/r06/relock_probe.txt:
+    after a lock, an unlock and new physical pages at the same addresses, an SDMA
+    copy through the new lock reads the OLD pages): units whose memory is replaced
+    between calls (munmap + mmap at the same address, as free + malloc can do) and
+    placed at a shifted extent each round, so every call's locks overlap the last
+    round's.  The library moves locked memory only with kernels (the gather /
+    scatter copy kernels), whose reads the probe shows right: every round's
+    outputs against the oracle, and the locked path really taken."""
+    code = REMAP.replace("ROOT", repr(ROOT))
+    env = dict(os.environ, ELECT_EC_REGISTER="1", ELECT_EC_ZEROCOPY="0")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0 and r.stdout.strip().startswith("OK"), r.stdout[-3000:] + r.stderr[-3000:]
+    st = json.loads(r.stdout.strip().split(" ", 1)[1])
+    assert st["unregister_failures"] == 0 and st["per_thread"] == 0 and st["registered"] >= 12, st
