@@ -1015,7 +1015,7 @@ struct DevicePolicy {
     bool env_read = false;
     std::vector<int> devices;  // empty: each thread's current device
     std::vector<int> nodes;    // NUMA node of each listed device (-1: unknown)
-    unsigned next[kMaxNumaNodes + 1] = {};  // round robin per NUMA node (the last: no node)
+    std::vector<unsigned> load;  // calling threads given each listed device (this generation)
     std::atomic<unsigned> generation{1};
 };
 
@@ -1073,24 +1073,28 @@ int thread_numa_node()
 }  // namespace
 
 // The device a thread on NUMA node `thread_node` gets from `devices` (their
-// nodes in `nodes`): round robin over the devices on its node when there is
-// one (counter next[node]), else over all of them (next[kMaxNumaNodes]).
+// nodes in `nodes`, the threads each already has in `load`): a least loaded
+// device, one on the thread's node when one of those is among the least loaded
+// (lowest index on ties).  So threads stay on their own socket while the
+// sockets' threads are about even, and unbound threads that all happen to run
+// on one socket at their first call still spread over every GPU: no device is
+// ever more than one thread ahead of another.
 // ELECT's one JVM per storage node runs concurrent_ec = 64 coding threads
 // (conf/elect.yaml:598) spread over every GPU; each thread's units are
 // allocated and filled by that thread (ECMessageVerbHandler.java:298-314), so
 // with first-touch placement they lie on its node, and a GPU on the same node
 // reads them without crossing the socket link (round 5's CPU baseline on one
 // box: 90.6 GiB/s from node 0 against 75.2 from node 1, BENCH_r05 cpu_baseline).
-int numa_pick(const int* devices, const int* nodes, int ndev, int thread_node, unsigned* next)
+int numa_pick(const int* devices, const int* nodes, int ndev, int thread_node, unsigned* load)
 {
-    int on_node = 0;
-    if (thread_node >= 0 && thread_node < kMaxNumaNodes)
-        for (int i = 0; i < ndev; ++i) on_node += nodes[i] == thread_node;
-    if (on_node == 0) return devices[next[kMaxNumaNodes]++ % static_cast<unsigned>(ndev)];
-    unsigned k = next[thread_node]++ % static_cast<unsigned>(on_node);
-    for (int i = 0; i < ndev; ++i)
-        if (nodes[i] == thread_node && k-- == 0) return devices[i];
-    return devices[0];  // (not reached)
+    int any = 0, local = -1;
+    for (int i = 0; i < ndev; ++i) {
+        if (load[i] < load[any]) any = i;
+        if (thread_node >= 0 && nodes[i] == thread_node && (local < 0 || load[i] < load[local])) local = i;
+    }
+    const int pick = local >= 0 && load[local] == load[any] ? local : any;
+    ++load[pick];
+    return devices[pick];
 }
 
 namespace {
@@ -1123,7 +1127,7 @@ void read_nodes(DevicePolicy& p)
     p.nodes.assign(p.devices.size(), -1);
     if (numa_policy())
         for (size_t i = 0; i < p.devices.size(); ++i) p.nodes[i] = device_numa_node(p.devices[i]);
-    for (unsigned& c : p.next) c = 0;
+    p.load.assign(p.devices.size(), 0);
 }
 
 thread_local int t_device = -1;
@@ -1146,7 +1150,7 @@ int host_device(int ndev, int* dev)
         }
         if (t_device < 0 || t_generation != p.generation.load()) {
             t_device = numa_pick(p.devices.data(), p.nodes.data(), static_cast<int>(p.devices.size()),
-                                 numa_policy() ? thread_numa_node() : -1, p.next);
+                                 numa_policy() ? thread_numa_node() : -1, p.load.data());
             t_generation = p.generation.load();
         }
     }
@@ -2373,8 +2377,12 @@ int host_device_map(const int* devices, const int* nodes, int ndev, const int* t
 {
     if (ndev <= 0 || nthreads < 0 || !devices || !nodes || (nthreads > 0 && (!thread_nodes || !out)))
         return ELECT_EC_EINVAL;
-    unsigned next[kMaxNumaNodes + 1] = {};
-    for (int t = 0; t < nthreads; ++t) out[t] = numa_pick(devices, nodes, ndev, thread_nodes[t], next);
+    try {
+        std::vector<unsigned> load(static_cast<size_t>(ndev), 0);
+        for (int t = 0; t < nthreads; ++t) out[t] = numa_pick(devices, nodes, ndev, thread_nodes[t], load.data());
+    } catch (const std::bad_alloc&) {
+        return ELECT_EC_ENOMEM;
+    }
     return ELECT_EC_OK;
 }
 
@@ -2394,6 +2402,7 @@ int set_host_devices(const int* devices, int n)
     } catch (const std::bad_alloc&) {
         p.devices.clear();
         p.nodes.clear();
+        p.load.clear();
         return ELECT_EC_ENOMEM;
     }
     p.generation++;  // threads pick a device again on their next call

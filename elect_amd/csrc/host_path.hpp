@@ -52,8 +52,8 @@ struct HostOp {
 int run_host(const HostOp& op, size_t len);
 int set_host_devices(const int* devices, int n);
 int device_numa_node(int dev);  // elect_ec_device_numa_node (-1: unknown)
-// The device a thread on NUMA node thread_node gets (host_device's choice; next: round-robin counters)
-int numa_pick(const int* devices, const int* nodes, int ndev, int thread_node, unsigned* next);
+// The device a thread on NUMA node thread_node gets (host_device's choice; load: threads per listed device)
+int numa_pick(const int* devices, const int* nodes, int ndev, int thread_node, unsigned* load);
 int host_device_map(const int* devices, const int* nodes, int ndev, const int* thread_nodes, int nthreads, int* out);
 int set_batching(int enable, unsigned window_us, size_t arena_bytes);
 int host_path_stats(uint64_t* out, int n);  // elect_ec_host_path_stats

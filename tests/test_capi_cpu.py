@@ -289,17 +289,31 @@ def test_numa_device_map():
     got = _lib.host_device_map(devs, nodes, threads)
     for t, d in enumerate(got):
         assert nodes[d] == threads[t], (t, d)  # every thread on a GPU of its own socket
-    for n in (0, 1):  # round robin within the node: each local GPU 8 threads
+    for n in (0, 1):  # least loaded within the node: each local GPU 8 threads
         mine = [d for d, x in zip(got, threads) if x == n]
         assert mine[:4] == [4 * n + i for i in range(4)]
         assert sorted(mine.count(d) for d in set(mine)) == [8, 8, 8, 8]
-    # a node without a listed GPU, or an unknown node, falls back to round robin over the whole list
+    # a node without a listed GPU, or an unknown node: the least loaded of the whole list
     assert _lib.host_device_map(devs, nodes, [2, 2, 2, -1, -1]) == [0, 1, 2, 3, 4]
-    # devices of unknown node (sysfs without NUMA info): plain round robin for every thread
+    # devices of unknown node (sysfs without NUMA info): round robin for every thread
     assert _lib.host_device_map([3, 5, 6], [-1, -1, -1], [0, 1, 0, 1]) == [3, 5, 6, 3]
     # a subset list (ELECT_EC_DEVICES=2,5): each socket's one GPU
     assert _lib.host_device_map([2, 5], [0, 1], [1, 0, 1, 0]) == [5, 2, 5, 2]
     # uneven sockets: 1 GPU on node 0, 3 on node 1
     assert _lib.host_device_map([0, 1, 2, 3], [0, 1, 1, 1], [0, 1, 1, 1, 1, 0]) == [0, 1, 2, 3, 1, 0]
+    # every thread on one socket at its first call (unbound threads can be): local GPUs first, but no GPU
+    # ever more than one thread ahead of another, so the other socket's GPUs still get their share
+    one_side = _lib.host_device_map(devs, nodes, [0] * 64)
+    counts = [one_side.count(d) for d in devs]
+    assert max(counts) - min(counts) <= 1, counts
+    assert one_side[:4] == [0, 1, 2, 3]  # the first four stay on their socket
     with pytest.raises(Exception):
         _lib.host_device_map([], [], [0])
+    # sockets uneven in threads (40 on node 0, 24 on node 1, arriving interleaved): balanced, and each
+    # thread local whenever a least loaded GPU is on its socket: 56 of the 64 (the most possible: 8 of
+    # node 0's threads must cross to even the load)
+    mixed = [1 if i % 8 in (2, 5, 7) else 0 for i in range(64)]
+    got = _lib.host_device_map(devs, nodes, mixed)
+    counts = [got.count(d) for d in devs]
+    assert max(counts) - min(counts) <= 1, counts
+    assert sum(nodes[d] == x for d, x in zip(got, mixed)) == 56
