@@ -121,13 +121,14 @@ int elect_ec_mix_probe(int num_in, int num_out, size_t chunk_size, size_t num_st
 int elect_ec_set_host_devices(const int* devices, int n);
 
 /* NUMA placement of the host-memory calls (round 6).  With a device list, a
- * calling thread is assigned, on its first call, a device of the list on its
- * own NUMA node (the node it runs on then, getcpu), round robin among those;
- * a thread on a node with no listed device takes the next of the whole list.
+ * calling thread is assigned, on its first call, a least-loaded device of the
+ * list (threads already assigned to it), one on its own NUMA node (the node it
+ * runs on then, getcpu) whenever one of those is among the least loaded; no
+ * device is ever more than one thread ahead of another.
  * ELECT's coding threads allocate and fill their units themselves
  * (ECMessageVerbHandler.java:298-314), so with first-touch placement a GPU on
  * the thread's node reads them without crossing the socket link.
- * ELECT_EC_NUMA=0 turns it off (plain round robin).
+ * ELECT_EC_NUMA=0 turns the node preference off.
  * elect_ec_device_numa_node: the node of a HIP device (its PCI function's
  * sysfs numa_node; -1 unknown).  elect_ec_host_device_map (diagnostics, no
  * device needed): the devices that threads on thread_nodes[0..num_threads)
