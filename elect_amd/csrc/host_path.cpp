@@ -1442,6 +1442,13 @@ private:
         hipEvent_t h2d_done = nullptr;
         hipEvent_t done_ev = nullptr;
         int64_t t_issue0 = 0, t_issue1 = 0, t_finish = 0;  // phase marks (now_ns, under the owner's mu_)
+        // early issue (Batcher::early_issue): the batch's gate number, written to the device
+        // counter behind its last gather (gate_written: that write is enqueued); the bytes its
+        // gathers move, and when the poller expects / saw its gate (now_ns)
+        uint64_t gate_seq = 0;
+        bool gate_written = false;
+        size_t gather_bytes = 0;
+        int64_t expect_gate = 0, t_gate = 0;
         bool h2d_landed = false;  // the batch in flight has passed its gate (under the owner's mu_)
         bool issued = false;      // ... and all of its work is enqueued, events recorded
 
@@ -1506,6 +1513,19 @@ private:
         // ran at 46 against 53 GB/s beside concurrent scatters: no faster than one
         // step.  tools/tune/spin_probe.cpp chain_*, profiles/r06/spin_chain.txt,
         // profiles/r06/pipeline_chain_ab.txt.)
+        if (early_issue()) {  // (without the counter, batches wait on the host for their gates)
+            hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&gate_ctr_), sizeof(uint64_t), hipMallocSignalMemory);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                e = hipMalloc(reinterpret_cast<void**>(&gate_ctr_), sizeof(uint64_t));
+            }
+            if (e == hipSuccess) e = hipMemset(gate_ctr_, 0, sizeof(uint64_t));
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                if (gate_ctr_) (void)hipFree(gate_ctr_);
+                gate_ctr_ = nullptr;
+            }
+        }
         for (Slab& s : active()) {
             s.owner = this;
             hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
@@ -1568,6 +1588,8 @@ private:
     // Frees whatever init() allocated (after a failed init: nothing is in flight).
     void release()
     {
+        if (gate_ctr_) (void)hipFree(gate_ctr_);
+        gate_ctr_ = nullptr;
         for (Slab& s : active()) {
             if (s.stream) (void)hipStreamDestroy(s.stream);
             s.stream = nullptr;
@@ -1621,8 +1643,18 @@ private:
                     if (x.state == Slab::kOpen && (!s || x.seq < s->seq)) s = &x;
                 return s != nullptr;
             });
+            uint64_t wait_for = 0;  // issue early: s's stream waits on the device for prev's gate number
             if (prev && prev->state == Slab::kInFlight) {  // asleep until the poller sees prev pass its gate
-                cv_worker_.wait(lock, [&] { return prev->h2d_landed || prev->state != Slab::kInFlight; });
+                auto passed = [&] { return prev->h2d_landed || prev->state != Slab::kInFlight; };
+                if (gate_ctr_ && prev->gate_written) {
+                    // ... or until shortly before it is expected to: s then leaves now and its
+                    // gathers start on the device right behind prev's (no poll / issue gap)
+                    const int64_t at = prev->expect_gate - static_cast<int64_t>(early_us()) * 1000;
+                    cv_worker_.wait_until(lock, std::chrono::steady_clock::time_point(std::chrono::nanoseconds(at)), passed);
+                    if (!passed()) wait_for = prev->gate_seq;
+                } else {
+                    cv_worker_.wait(lock, passed);
+                }
             } else {
                 const unsigned w = batch_config().window_us.load();
                 if (w) cv_worker_.wait_until(lock, s->opened + std::chrono::microseconds(w), [&] { return s->full; });
@@ -1647,7 +1679,9 @@ private:
             s->t_issue1 = 0;
             lock.unlock();
             const uint64_t t0 = thread_cpu_ns();
-            const hipError_t e = shape.direct ? issue_direct(*s, shape, n, slots_) : issue_staged(*s, shape, n);
+            s->gate_written = false;
+            const hipError_t e = shape.direct ? issue_direct(*s, shape, n, slots_, wait_for)
+                                              : issue_staged(*s, shape, n, wait_for);
             g_issue_cpu_ns.fetch_add(thread_cpu_ns() - t0);
             if (e != hipSuccess) drain(*s);  // no completion was queued: nothing of it may still run
             const int64_t t_issued = now_ns();
@@ -1655,6 +1689,9 @@ private:
             g_batches.fetch_add(1, std::memory_order_relaxed);
             lock.lock();
             s->t_issue1 = t_issued;
+            // when its gate should pass: its gathers start at issue end or behind prev's gate
+            const int64_t start = std::max<int64_t>(t_issued, wait_for && prev ? prev->expect_gate : 0);
+            s->expect_gate = start + static_cast<int64_t>(static_cast<double>(s->gather_bytes) * gate_ns_per_byte_);
             if (e != hipSuccess) {
                 finish(s, map_hip(e));
             } else {
@@ -1831,13 +1868,64 @@ private:
         return true;
     }
 
+    // ---- early issue (round 6) ---------------------------------------------------
+    // A batch leaves when the previous batch has passed its gate (the poller saw its
+    // gathers done): ~30-130 us of the link unused per batch between one batch's last
+    // gather and the next one's first (poll interval, dispatcher wake, issue, launch;
+    // 8 callers: ~70 us of each ~1.35 ms batch, profiles/r06/early_issue_ab.txt).  With
+    // early issue (ELECT_EC_EARLY_ISSUE, default on) the dispatcher closes the next batch
+    // ELECT_EC_EARLY_US (default 150) before the previous batch's gate is expected (its
+    // gather bytes at the measured gather time per byte), and the new batch's stream first
+    // waits on the device until the previous batch has written its gate number behind its
+    // last gather (hipStreamWriteValue64 / hipStreamWaitValue64 on one counter per device:
+    // the command processor waits, no host thread spins, profiles/r06/spin_chain.txt).  A
+    // wait is enqueued only for a number whose write was enqueued.
+    static bool early_issue()
+    {
+        static const bool on = [] {
+            const char* e = std::getenv("ELECT_EC_EARLY_ISSUE");
+            return !(e && std::atoi(e) == 0);
+        }();
+        return on;
+    }
+    static unsigned early_us()
+    {
+        static const unsigned u = [] {
+            const char* e = std::getenv("ELECT_EC_EARLY_US");
+            return e ? static_cast<unsigned>(std::max(0, std::atoi(e))) : 150u;
+        }();
+        return u;
+    }
+    hipError_t wait_before(Slab& s, uint64_t wait_for) const
+    {
+        if (!wait_for) return hipSuccess;
+        return hipStreamWaitValue64(s.stream, gate_ctr_, wait_for, hipStreamWaitValueGte, ~uint64_t{0});
+    }
+    // The gate: (early issue) the gate number written for the next batch's stream, then the
+    // host-visible event the poller queries.  In that order: a batch the dispatcher issues
+    // without a device wait (the previous one seen past its gate) writes its own, higher
+    // number only after the previous number has landed, so the counter never goes back.
+    // Written only while other callers wait (a lone caller's next batch never overlaps).
+    hipError_t record_gate(Slab& s, int n)
+    {
+        hipError_t e = hipSuccess;
+        s.gate_written = false;
+        if (gate_ctr_ && callers_.load(std::memory_order_relaxed) > n) {
+            s.gate_seq = ++gate_seq_;
+            e = hipStreamWriteValue64(s.stream, gate_ctr_, s.gate_seq, 0);
+            s.gate_written = e == hipSuccess;
+        }
+        if (e == hipSuccess) e = hipEventRecord(s.h2d_done, s.stream);
+        return e;
+    }
+
     // Direct batches: each unit's [lo, hi) straight from / to its caller's
     // page-locked memory (a locked pageable unit's interior pages, or a pool
     // unit), the rest (a locked unit's partial end pages) through the arena; by
     // gather / scatter kernels reading the piece table where it lies.  s's
     // buffers, stream and events never change after init(); its shape comes from
     // the copy taken under mu_.
-    hipError_t issue_direct(Slab& s, const Shape& sh, int n, const DirectSlots& d)
+    hipError_t issue_direct(Slab& s, const Shape& sh, int n, const DirectSlots& d, uint64_t wait_for)
     {
         Steps st = plan_steps(sh, n, d);
         size_t begin[kMaxSteps + 2];
@@ -1856,15 +1944,18 @@ private:
                         l[q * sh.cols + j] = static_cast<uint32_t>(raw > w0 ? std::min(raw - w0, w) : 0);
                     }
             }
-        hipError_t e = hipSuccess;
+        s.gather_bytes = 0;
+        for (size_t k = 0; k < static_cast<size_t>(st.n); ++k)  // (whole stages: pieces of both directions)
+            for (size_t i = begin[k]; i < begin[k + 1]; ++i) s.gather_bytes += s.pieces[i].n;
+        hipError_t e = wait_before(s, wait_for);
         const bool seed = sh.hashed && st.n > 1;  // windows add into entries seeded 31^len
-        if (seed)
+        if (seed && e == hipSuccess)
             e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_hash), static_cast<int>(kern::pow31(sh.len)),
                                   static_cast<size_t>(n) * sh.rows, s.stream);
         for (int k = 0; k <= st.n && e == hipSuccess; ++k) {
             e = kern::launch_copy_pieces(s.pieces_dev + begin[k], static_cast<uint32_t>(begin[k + 1] - begin[k]), s.stream);
             // the gate: the batch's last gather is done (the next batch's gathers may start beside its last scatter)
-            if (e == hipSuccess && k == st.n - 1) e = hipEventRecord(s.h2d_done, s.stream);
+            if (e == hipSuccess && k == st.n - 1) e = record_gate(s, n);
             if (e != hipSuccess || k == st.n) break;
             const size_t w0 = k * st.window, w = std::min(sh.len, w0 + st.window) - w0;
             ApplyParams p;
@@ -1898,15 +1989,17 @@ private:
 
     // Staged batches (the callers copied their units into the pinned arena): one
     // H2D, one coding launch over the arena's tiles, one D2H.
-    hipError_t issue_staged(Slab& s, const Shape& sh, int n)
+    hipError_t issue_staged(Slab& s, const Shape& sh, int n, uint64_t wait_for)
     {
         const size_t in_stride = sh.tiles * sh.cols * sh.pitch;  // per slot
         const size_t out_stride = sh.tiles * sh.rows * sh.pitch;
-        hipError_t e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
+        s.gather_bytes = n * in_stride;
+        hipError_t e = wait_before(s, wait_for);
+        if (e == hipSuccess) e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
         if (e == hipSuccess && sh.padded)
             e = hipMemcpyAsync(s.d_lens, s.pin_lens, static_cast<size_t>(n) * sh.cols * sizeof(uint32_t),
                                hipMemcpyHostToDevice, s.stream);
-        if (e == hipSuccess) e = hipEventRecord(s.h2d_done, s.stream);
+        if (e == hipSuccess) e = record_gate(s, n);
         if (e == hipSuccess) {
             // coding stripes: the slots' tiles in order (untiled: the slots)
             ApplyParams p;
@@ -1992,6 +2085,14 @@ private:
                 lock.lock();
                 if (!landed && eh != hipErrorNotReady) {
                     x.h2d_landed = true;
+                    x.t_gate = now_ns();
+                    // the gather time per byte, for the next batches' expected gates (from the later of
+                    // issue end and the previous gate: a batch issued early starts behind it)
+                    const int64_t from = std::max(x.t_issue1, last_gate_);
+                    if (x.t_issue1 && x.gather_bytes > (size_t{1} << 20) && x.t_gate > from)
+                        gate_ns_per_byte_ = 0.8 * gate_ns_per_byte_ +
+                                            0.2 * static_cast<double>(x.t_gate - from) / static_cast<double>(x.gather_bytes);
+                    last_gate_ = x.t_gate;
                     cv_worker_.notify_one();
                 }
                 if (eh != hipSuccess && eh != hipErrorNotReady) {  // a failed batch is done, with its error
@@ -2032,6 +2133,13 @@ private:
     std::condition_variable cv_poll_;    // the poller, while no batch is in flight
     DirectSlots slots_;                  // the dispatcher's copy of a direct batch's slots (its thread only)
     std::vector<kern::CopyPiece> gbuf_, sbuf_;  // a stage's gather / scatter pieces (dispatcher thread only)
+    // early issue: the device counter each batch writes its gate number to behind its last gather
+    // (a batch issued early waits on it, hipStreamWaitValue64), the last number handed out
+    // (dispatcher thread), and the measured gather time per byte (EWMA, under mu_)
+    uint64_t* gate_ctr_ = nullptr;
+    uint64_t gate_seq_ = 0;
+    double gate_ns_per_byte_ = 1.0 / 50.0;
+    int64_t last_gate_ = 0;  // when the poller last saw a gate pass (under mu_)
     std::condition_variable cv_slot_;    // callers waiting for an arena to reserve in
     bool started_ = false;
     bool init_failed_ = false;  // the arenas could not be allocated: every call runs directly
