@@ -8,6 +8,7 @@
 
 #include <emmintrin.h>
 #include <pthread.h>
+#include <sys/prctl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -1449,6 +1450,9 @@ private:
         bool gate_written = false;
         size_t gather_bytes = 0;
         int64_t expect_gate = 0, t_gate = 0;
+        // the bytes moved after the gate, and when the poller expects the batch done
+        size_t tail_bytes = 0;
+        int64_t expect_done = 0;
         bool h2d_landed = false;  // the batch in flight has passed its gate (under the owner's mu_)
         bool issued = false;      // ... and all of its work is enqueued, events recorded
 
@@ -1632,6 +1636,7 @@ private:
     void worker()
     {
         pthread_setname_np(pthread_self(), ("ec-dispatch" + std::to_string(dev_)).c_str());
+        set_timer_slack();
         (void)hipSetDevice(dev_);
         Slab* prev = nullptr;
         std::unique_lock<std::mutex> lock(mu_);
@@ -1724,9 +1729,16 @@ private:
     // lens arrays, moved by the first stage), hashed ops adding each window's
     // terms (31^(window offset + i)) into entries seeded 31^len.
     struct Steps {
-        int n = 1;          // steps
-        size_t window = 0;  // unit bytes per step (the last takes the rest)
-        size_t piece = 0;   // gather / scatter piece bytes
+        int n = 1;                     // steps
+        size_t at[kMaxSteps + 1] = {};  // window k is unit bytes [at[k], at[k + 1])
+        size_t piece = 0;              // gather / scatter piece bytes
+        static Steps one(size_t len, size_t piece)
+        {
+            Steps st;
+            st.at[1] = len;
+            st.piece = piece;
+            return st;
+        }
     };
     static constexpr size_t kMinWindow = size_t{256} << 10;
     static constexpr size_t kMinPiece = size_t{16} << 10;
@@ -1770,6 +1782,17 @@ private:
     // against 39.4-40.6 / 42.2-43.9 / 44.2-45.5 in one step, one caller 29.5-30.3
     // against 27.1-29.4 on the same box (35.0 against 28.4-29.2 on another),
     // profiles/r06/pipeline_ab.txt.
+    // ELECT_EC_TAPER (default 1): the last two windows a half and a quarter of the others
+    // (profiles/r06/taper_ab.txt); 0: equal windows.
+    static bool taper()
+    {
+        static const bool t = [] {
+            const char* e = std::getenv("ELECT_EC_TAPER");
+            return !(e && std::atoi(e) == 0);
+        }();
+        return t;
+    }
+
     static bool pipeline_alone_only()
     {
         static const bool a = [] {
@@ -1788,10 +1811,22 @@ private:
         if (pipeline_alone_only() && callers_.load() > n) s = 1;  // other callers wait: batches overlap instead
         s = static_cast<int>(std::min<size_t>(s, std::max<size_t>(1, sh.len / kMinWindow)));
         if (sh.padded) s = static_cast<int>(std::min<size_t>(s, std::max<size_t>(1, kMetaEntries / (static_cast<size_t>(n) * sh.cols))));
+        // window weights: equal, or (taper) 4 : ... : 4 : 2 : 1, so that the scatter left
+        // after the last gather is a small window's
+        unsigned wt[kMaxSteps], total = 0;
+        for (int k = 0; k < s; ++k) total += wt[k] = !taper() || k + 2 < s ? 4u : k + 2 == s ? 2u : 1u;
         Steps st;
+        st.n = 0;
         constexpr size_t kAlign = size_t{1} << 16;
-        st.window = s > 1 ? ((sh.len + s - 1) / s + kAlign - 1) / kAlign * kAlign : sh.len;
-        st.n = static_cast<int>((sh.len + st.window - 1) / st.window);
+        unsigned cum = 0;
+        for (int k = 0; k < s; ++k) {  // boundaries on 64 KiB multiples, never an empty window
+            cum += wt[k];
+            size_t b = k + 1 == s ? sh.len
+                                  : (sh.len / total * cum + sh.len % total * cum / total + kAlign / 2) / kAlign * kAlign;
+            if (b > sh.len) b = sh.len;
+            if (b > st.at[st.n]) st.at[++st.n] = b;
+        }
+        if (st.n == 0) st = Steps::one(sh.len, 0);
         st.piece = piece_for((in_bytes + static_cast<size_t>(n) * sh.rows * sh.len) / st.n);
         return st;
     }
@@ -1804,8 +1839,31 @@ private:
     static bool write_pieces(Slab& s, const Shape& sh, int n, const DirectSlots& d, const Steps& st, size_t* begin,
                              std::vector<kern::CopyPiece>& gbuf, std::vector<kern::CopyPiece>& sbuf)
     {
-        const size_t in_stride = sh.cols * sh.pitch, out_stride = sh.rows * sh.pitch;
         size_t np = 0;
+        for (int k = 0; k <= st.n; ++k) {
+            begin[k] = np;
+            if (!write_stage(s, sh, n, d, st, k, np, gbuf, sbuf)) return false;
+        }
+        begin[st.n + 1] = np;
+        return true;
+    }
+    // At least the number of pieces write_pieces() writes for `st` (a unit's range
+    // clipped to a window is at most three segments, each ceil(bytes / piece)).
+    static size_t piece_bound(const Shape& sh, int n, const Steps& st)
+    {
+        size_t b = 0;
+        for (int k = 0; k <= st.n; ++k) {
+            if (k < st.n) b += static_cast<size_t>(n) * sh.cols * ((st.at[k + 1] - st.at[k]) / st.piece + 3);
+            if (k >= 1) b += static_cast<size_t>(n) * sh.rows * ((st.at[k] - st.at[k - 1]) / st.piece + 3);
+        }
+        if (sh.padded) b += static_cast<size_t>(st.n) * n * sh.cols * sizeof(uint32_t) / st.piece + 1;
+        return b + 1;  // (+1: the hashes)
+    }
+    // Stage k's pieces at s.pieces[np...), np advanced past them.
+    static bool write_stage(Slab& s, const Shape& sh, int n, const DirectSlots& d, const Steps& st, int k, size_t& np,
+                            std::vector<kern::CopyPiece>& gbuf, std::vector<kern::CopyPiece>& sbuf)
+    {
+        const size_t in_stride = sh.cols * sh.pitch, out_stride = sh.rows * sh.pitch;
         bool room = true;  // (the lists never grow past what init() reserved: no allocation here)
         auto put = [&](std::vector<kern::CopyPiece>& v, const uint8_t* from, uint8_t* to, size_t bytes) {
             for (size_t o = 0; o < bytes && room; o += st.piece) {
@@ -1819,11 +1877,11 @@ private:
             const size_t x = std::max(a, w0), y = std::min(b, w1);
             if (x < y) put(v, from + x, to + x, y - x);
         };
-        for (int k = 0; k <= st.n; ++k) {
+        {
             gbuf.clear();
             sbuf.clear();
             if (k < st.n) {  // gather window k
-                const size_t w0 = k * st.window, w1 = std::min(sh.len, w0 + st.window);
+                const size_t w0 = st.at[k], w1 = st.at[k + 1];
                 if (k == 0 && sh.padded)  // the per-step content lengths ride in the first stage
                     put(gbuf, s.pin_lens_dev, reinterpret_cast<uint8_t*>(s.d_lens),
                         static_cast<size_t>(st.n) * n * sh.cols * sizeof(uint32_t));
@@ -1839,7 +1897,7 @@ private:
                     }
             }
             if (k >= 1) {  // scatter window k-1
-                const size_t w0 = (k - 1) * st.window, w1 = std::min(sh.len, w0 + st.window);
+                const size_t w0 = st.at[k - 1], w1 = st.at[k];
                 for (int q = 0; q < n; ++q)
                     for (int r = 0; r < sh.rows; ++r) {
                         const size_t i = static_cast<size_t>(q) * kern::kMaxRows + r;
@@ -1854,7 +1912,6 @@ private:
                     put(sbuf, reinterpret_cast<const uint8_t*>(s.d_hash), s.pin_hash_dev,
                         static_cast<size_t>(n) * sh.rows * sizeof(int32_t));
             }
-            begin[k] = np;
             if (!room || np + gbuf.size() + sbuf.size() > s.max_pieces) return false;
             // interleave: piece i of a list of m sits at position (i + 0.5) / m of the stage
             size_t gi = 0, si = 0;
@@ -1864,7 +1921,6 @@ private:
                 s.pieces[np++] = take_g ? gbuf[gi++] : sbuf[si++];
             }
         }
-        begin[st.n + 1] = np;
         return true;
     }
 
@@ -1929,14 +1985,24 @@ private:
     {
         Steps st = plan_steps(sh, n, d);
         size_t begin[kMaxSteps + 2];
-        if (!write_pieces(s, sh, n, d, st, begin, gbuf_, sbuf_)) {
-            st = Steps{1, sh.len, kern::kMaxPieceBytes};  // one step of 64 KiB pieces always fits
+        // A pipelined batch's table is written stage by stage, each just before its
+        // launch, so that the first gather starts after one stage's descriptors, not
+        // all of them (when the table surely has room for all).
+        static const bool stage_writes = [] {  // ELECT_EC_STAGE_WRITES=0: the whole table first (A/B)
+            const char* e = std::getenv("ELECT_EC_STAGE_WRITES");
+            return !(e && std::atoi(e) == 0);
+        }();
+        const bool by_stage = stage_writes && st.n > 1 && piece_bound(sh, n, st) <= s.max_pieces;
+        if (by_stage) {
+            begin[0] = 0;
+        } else if (!write_pieces(s, sh, n, d, st, begin, gbuf_, sbuf_)) {
+            st = Steps::one(sh.len, kern::kMaxPieceBytes);  // one step of 64 KiB pieces always fits
             if (!write_pieces(s, sh, n, d, st, begin, gbuf_, sbuf_)) return hipErrorInvalidValue;
         }
         const size_t in_stride = sh.cols * sh.pitch, out_stride = sh.rows * sh.pitch;
         if (sh.padded)  // [step][slot][col]: each window's share of every unit's content
             for (int t = 0; t < st.n; ++t) {
-                const size_t w0 = t * st.window, w = std::min(sh.len, w0 + st.window) - w0;
+                const size_t w0 = st.at[t], w = st.at[t + 1] - w0;
                 uint32_t* l = s.pin_lens + static_cast<size_t>(t) * n * sh.cols;
                 for (int q = 0; q < n; ++q)
                     for (int j = 0; j < sh.cols; ++j) {
@@ -1944,20 +2010,33 @@ private:
                         l[q * sh.cols + j] = static_cast<uint32_t>(raw > w0 ? std::min(raw - w0, w) : 0);
                     }
             }
-        s.gather_bytes = 0;
-        for (size_t k = 0; k < static_cast<size_t>(st.n); ++k)  // (whole stages: pieces of both directions)
-            for (size_t i = begin[k]; i < begin[k + 1]; ++i) s.gather_bytes += s.pieces[i].n;
+        s.gather_bytes = 0;  // (whole stages up to the last gather: pieces of both directions)
+        auto stage_bytes = [&](int k) {
+            if (k < st.n)
+                for (size_t i = begin[k]; i < begin[k + 1]; ++i) s.gather_bytes += s.pieces[i].n;
+        };
+        if (!by_stage)
+            for (int k = 0; k < st.n; ++k) stage_bytes(k);
         hipError_t e = wait_before(s, wait_for);
         const bool seed = sh.hashed && st.n > 1;  // windows add into entries seeded 31^len
         if (seed && e == hipSuccess)
             e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.d_hash), static_cast<int>(kern::pow31(sh.len)),
                                   static_cast<size_t>(n) * sh.rows, s.stream);
         for (int k = 0; k <= st.n && e == hipSuccess; ++k) {
+            if (by_stage) {
+                size_t np = begin[k];
+                if (!write_stage(s, sh, n, d, st, k, np, gbuf_, sbuf_)) {
+                    e = hipErrorInvalidValue;  // (piece_bound() said it fits: not reached)
+                    break;
+                }
+                begin[k + 1] = np;
+                stage_bytes(k);
+            }
             e = kern::launch_copy_pieces(s.pieces_dev + begin[k], static_cast<uint32_t>(begin[k + 1] - begin[k]), s.stream);
             // the gate: the batch's last gather is done (the next batch's gathers may start beside its last scatter)
             if (e == hipSuccess && k == st.n - 1) e = record_gate(s, n);
             if (e != hipSuccess || k == st.n) break;
-            const size_t w0 = k * st.window, w = std::min(sh.len, w0 + st.window) - w0;
+            const size_t w0 = st.at[k], w = st.at[k + 1] - w0;
             ApplyParams p;
             p.len = w;
             p.stripes = static_cast<uint64_t>(n);
@@ -1983,6 +2062,9 @@ private:
             }
             e = kern::launch_apply(p, s.stream);
         }
+        s.tail_bytes = 0;
+        if (e == hipSuccess)
+            for (size_t i = begin[st.n]; i < begin[st.n + 1]; ++i) s.tail_bytes += s.pieces[i].n;
         if (e == hipSuccess) e = hipEventRecord(s.done_ev, s.stream);
         return e;
     }
@@ -1994,6 +2076,7 @@ private:
         const size_t in_stride = sh.tiles * sh.cols * sh.pitch;  // per slot
         const size_t out_stride = sh.tiles * sh.rows * sh.pitch;
         s.gather_bytes = n * in_stride;
+        s.tail_bytes = n * out_stride;
         hipError_t e = wait_before(s, wait_for);
         if (e == hipSuccess) e = hipMemcpyAsync(s.d_in, s.pin_in, n * in_stride, hipMemcpyHostToDevice, s.stream);
         if (e == hipSuccess && sh.padded)
@@ -2049,6 +2132,18 @@ private:
     // alone was 19-20 core-ms per GiB, and the dispatcher spinning on the H2D
     // event 53 against 35 (hostpath_register_ab.txt E); both modes were A/B
     // switches in round 5 (ELECT_EC_DISPATCH_WAIT) and are gone since.
+    // The poller's sleeps and the dispatcher's timed waits end up to the thread's timer
+    // slack late (Linux default 50 us): a 25 us poll round took ~75 us, and a lone caller's
+    // call waited for the round after its batch was done.  ELECT_EC_TIMER_SLACK_NS (default
+    // 2000; 0 leaves the default) for these two threads only (profiles/r06/slack_ab.txt).
+    static void set_timer_slack()
+    {
+        static const long ns = [] {
+            const char* e = std::getenv("ELECT_EC_TIMER_SLACK_NS");
+            return e ? std::max(0L, std::atol(e)) : 2000L;
+        }();
+        if (ns > 0) (void)prctl(PR_SET_TIMERSLACK, static_cast<unsigned long>(ns), 0, 0, 0);
+    }
     static unsigned poll_us()
     {
         static const unsigned u = [] {
@@ -2065,6 +2160,7 @@ private:
     void poller()
     {
         pthread_setname_np(pthread_self(), ("ec-poll" + std::to_string(dev_)).c_str());
+        set_timer_slack();
         (void)hipSetDevice(dev_);
         std::unique_lock<std::mutex> lock(mu_);
         for (;;) {
@@ -2093,6 +2189,7 @@ private:
                         gate_ns_per_byte_ = 0.8 * gate_ns_per_byte_ +
                                             0.2 * static_cast<double>(x.t_gate - from) / static_cast<double>(x.gather_bytes);
                     last_gate_ = x.t_gate;
+                    x.expect_done = x.t_gate + static_cast<int64_t>(static_cast<double>(x.tail_bytes) * tail_ns_per_byte_);
                     cv_worker_.notify_one();
                 }
                 if (eh != hipSuccess && eh != hipErrorNotReady) {  // a failed batch is done, with its error
@@ -2100,12 +2197,41 @@ private:
                     continue;
                 }
                 if (ed == hipErrorNotReady) continue;
+                if (ed == hipSuccess && x.tail_bytes > (size_t{256} << 10)) {
+                    const int64_t t = now_ns();
+                    tail_ns_per_byte_ = 0.8 * tail_ns_per_byte_ +
+                                        0.2 * static_cast<double>(t - x.t_gate) / static_cast<double>(x.tail_bytes);
+                }
                 finish(&x, ed == hipSuccess ? ELECT_EC_OK : map_hip(ed));
             }
+            const int64_t wake = next_poll(now_ns());
             lock.unlock();
-            std::this_thread::sleep_for(std::chrono::microseconds(poll_us()));
+            std::this_thread::sleep_until(std::chrono::steady_clock::time_point(std::chrono::nanoseconds(wake)));
             lock.lock();
         }
+    }
+
+    // When the poller looks next (mu_ held): poll_us() from now, or earlier when a batch
+    // in flight nears the time its next event (gate, then done) is expected, and every
+    // ELECT_EC_POLL_FINE_US (default 5) from then on until that event is seen.  A lone
+    // caller's call no longer waits up to a whole round after its batch is done.
+    int64_t next_poll(int64_t now) const
+    {
+        static const int64_t fine = [] {
+            const char* e = std::getenv("ELECT_EC_POLL_FINE_US");
+            return static_cast<int64_t>(e ? std::max(0, std::atoi(e)) : 5) * 1000;
+        }();
+        int64_t wake = now + static_cast<int64_t>(poll_us()) * 1000;
+        if (!fine) return wake;
+        for (int i = 0; i < nslabs_; ++i) {
+            const Slab& x = slabs_[i];
+            if (x.state != Slab::kInFlight || !x.issued) continue;
+            const int64_t target = x.h2d_landed ? x.expect_done : x.expect_gate;
+            const int64_t base = x.h2d_landed ? x.t_gate : x.t_issue1;
+            const int64_t start = target - std::max<int64_t>(10000, (target - base) / 8);
+            wake = std::min(wake, now >= start ? now + fine : start);
+        }
+        return wake;
     }
 
     void finish(Slab* s, int status)  // mu_ held
@@ -2139,6 +2265,7 @@ private:
     uint64_t* gate_ctr_ = nullptr;
     uint64_t gate_seq_ = 0;
     double gate_ns_per_byte_ = 1.0 / 50.0;
+    double tail_ns_per_byte_ = 1.0 / 50.0;  // after the gate, to done (poller only)
     int64_t last_gate_ = 0;  // when the poller last saw a gate pass (under mu_)
     std::condition_variable cv_slot_;    // callers waiting for an arena to reserve in
     bool started_ = false;

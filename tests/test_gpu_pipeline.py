@@ -115,6 +115,7 @@ CONFIGS = {
     "three_steps": {"ELECT_EC_PIPELINE_STEPS": "3", "ELECT_EC_STEP_KB": "256"},
     "eight_steps_64k_pieces": {"ELECT_EC_PIPELINE_STEPS": "8", "ELECT_EC_STEP_KB": "256", "ELECT_EC_PIECE_KB": "64"},
     "eight_steps_16k_pieces": {"ELECT_EC_PIPELINE_STEPS": "8", "ELECT_EC_STEP_KB": "256", "ELECT_EC_PIECE_KB": "16"},
+    "five_equal_windows_whole_table": {"ELECT_EC_PIPELINE_STEPS": "5", "ELECT_EC_TAPER": "0", "ELECT_EC_STAGE_WRITES": "0"},
 }
 
 
