@@ -194,3 +194,54 @@ def test_zero_copy_content_end_on_page_boundary():
     import json
     st = json.loads(r.stdout.strip().split(" ", 1)[1])
     assert st["zero_copy"] == 2 and st["zero_copy_fallback"] == 0, st
+
+
+MIXED_POOL = r"""
+import json, sys
+import numpy as np
+import torch
+sys.path.insert(0, ROOT)
+from elect_amd import _lib
+from elect_amd.coder import RSCoder
+from oracle import ec_oracle as orc
+
+torch.cuda.init()
+rng = np.random.default_rng(21)
+k, m, L = 4, 2, 4404020
+c = RSCoder(k, m)
+enc = orc.Encoder(k, m)
+pool = [_lib.HostBuffer(L) for _ in range(2)]  # data unit 1 and parity unit 0 in page-locked pool blocks
+bad = []
+for it in range(3):
+    d = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    pool[0].array[:] = d[1]
+    d[1] = pool[0].array
+    p = [pool[1].array, np.zeros(L, np.uint8)]
+    p[0][:] = 0
+    c.encode_host([x.ctypes.data for x in d], [x.ctypes.data for x in p], L)
+    want = enc.encode(d)
+    bad += [f"encode {it} parity {r}" for r in range(m) if not np.array_equal(p[r], want[r])]
+    out = [np.zeros(L, np.uint8)]
+    c.decode_host([p[0].ctypes.data, d[1].ctypes.data, d[2].ctypes.data, d[3].ctypes.data], [4, 1, 2, 3], [0],
+                  [out[0].ctypes.data], L)
+    if not np.array_equal(out[0], d[0]):
+        bad.append(f"decode {it}")
+# the pool blocks are still page-locked and move right through the batched path afterwards
+if not all(_lib.host_pinned(b.addr, L) for b in pool):
+    bad.append("pool block no longer pinned")
+print("BAD " + "; ".join(bad) if bad else "OK", json.dumps(_lib.host_path_stats()))
+"""
+
+
+def test_zero_copy_pool_units_among_pageable_ones():
+    """a zero-copy call whose units mix pool blocks and pageable memory must
+    not lock (and later unlock) the pool's pages itself: the pool units are addressed through the
+    pool's own device mapping, the pageable ones locked for the call.  No failed unlock, and the
+    pool blocks stay locked and usable afterwards (the second and third rounds reuse them)."""
+    code = MIXED_POOL.replace("ROOT", repr(ROOT))
+    env = dict(os.environ, ELECT_EC_ZEROCOPY="2")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0 and r.stdout.strip().startswith("OK"), r.stdout[-2000:] + r.stderr[-2000:]
+    import json
+    st = json.loads(r.stdout.strip().split(" ", 1)[1])
+    assert st["zero_copy"] == 6 and st["zero_copy_fallback"] == 0 and st["unregister_failures"] == 0, st
