@@ -78,6 +78,8 @@ SIGNATURES = [
     ("elect_ec_device_numa_node", ctypes.c_int, [ctypes.c_int, _ip]),
     ("elect_ec_host_device_map", ctypes.c_int, [_ip, _ip, ctypes.c_int, _ip, ctypes.c_int, _ip]),
     ("elect_ec_set_batching", ctypes.c_int, [ctypes.c_int, ctypes.c_uint, ctypes.c_size_t]),
+    ("elect_ec_internal_pipeline_windows", ctypes.c_int, [ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                                          ctypes.POINTER(ctypes.c_size_t), _ip]),
     ("elect_ec_host_path_stats", ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     ("elect_ec_mix_probe", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
                                           ctypes.POINTER(ColumnT), _cp, ctypes.POINTER(ColumnT), ctypes.c_int,
@@ -257,6 +259,15 @@ def host_device_map(devices, device_nodes, thread_nodes) -> list:
                                        int_array(thread_nodes) if thread_nodes else None, len(thread_nodes), out),
           "host_device_map")
     return list(out[:len(thread_nodes)])
+
+
+def pipeline_windows(length: int, steps: int, taper: bool = True) -> list:
+    """Window boundaries [0, ..., length] a lone call's units of `length` bytes are pipelined over
+    in at most `steps` steps (the library's plan; a test hook, not part of include/elect_ec.h)."""
+    at = (ctypes.c_size_t * (steps + 1))()
+    n = ctypes.c_int()
+    check(lib.elect_ec_internal_pipeline_windows(length, steps, int(taper), at, ctypes.byref(n)), "pipeline_windows")
+    return list(at[:n.value + 1])
 
 
 def host_path_stats() -> dict:

@@ -325,6 +325,15 @@ int elect_ec_host_device_map(const int* devices, const int* device_nodes, int nu
     return elect::host::host_device_map(devices, device_nodes, num_devices, thread_nodes, num_threads, out);
 }
 
+// Test hook, not part of include/elect_ec.h: the windows a lone call of units of len bytes
+// is pipelined over (host_path.cpp pipeline_windows); bounds: steps + 1 entries.
+int elect_ec_internal_pipeline_windows(size_t len, int steps, int taper, size_t* bounds, int* n)
+{
+    if (!bounds || !n || steps < 1 || steps > 64) return ELECT_EC_EINVAL;
+    *n = elect::host::pipeline_windows(len, steps, taper != 0, bounds);
+    return ELECT_EC_OK;
+}
+
 int elect_ec_set_batching(int enable, unsigned window_us, size_t arena_bytes)
 {
     return elect::host::set_batching(enable, window_us, arena_bytes);

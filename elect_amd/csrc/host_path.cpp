@@ -365,6 +365,31 @@ int64_t now_ns()
 }
 
 // ELECT_EC_PHASE_DEBUG=<us>: report calls whose fill phase took longer (diagnostics)
+}  // namespace
+
+// Window weights equal, or (taper) 4 : ... : 4 : 2 : 1, so that the scatter left after the
+// last gather is a small window's; boundaries on 64 KiB multiples, never an empty window.
+int pipeline_windows(size_t len, int steps, bool taper, size_t* at)
+{
+    steps = std::max(1, steps);
+    unsigned total = 0;
+    for (int k = 0; k < steps; ++k) total += !taper || k + 2 < steps ? 4u : k + 2 == steps ? 2u : 1u;
+    constexpr size_t kAlign = size_t{1} << 16;
+    int n = 0;
+    unsigned cum = 0;
+    at[0] = 0;
+    for (int k = 0; k < steps; ++k) {
+        cum += !taper || k + 2 < steps ? 4u : k + 2 == steps ? 2u : 1u;
+        size_t b = k + 1 == steps ? len : (len / total * cum + len % total * cum / total + kAlign / 2) / kAlign * kAlign;
+        if (b > len) b = len;
+        if (b > at[n]) at[++n] = b;
+    }
+    if (n == 0) at[n = 1] = len;  // (len 0: one empty window)
+    return n;
+}
+
+namespace {
+
 int64_t phase_debug()
 {
     static const int64_t ns = [] {
@@ -1811,22 +1836,8 @@ private:
         if (pipeline_alone_only() && callers_.load() > n) s = 1;  // other callers wait: batches overlap instead
         s = static_cast<int>(std::min<size_t>(s, std::max<size_t>(1, sh.len / kMinWindow)));
         if (sh.padded) s = static_cast<int>(std::min<size_t>(s, std::max<size_t>(1, kMetaEntries / (static_cast<size_t>(n) * sh.cols))));
-        // window weights: equal, or (taper) 4 : ... : 4 : 2 : 1, so that the scatter left
-        // after the last gather is a small window's
-        unsigned wt[kMaxSteps], total = 0;
-        for (int k = 0; k < s; ++k) total += wt[k] = !taper() || k + 2 < s ? 4u : k + 2 == s ? 2u : 1u;
         Steps st;
-        st.n = 0;
-        constexpr size_t kAlign = size_t{1} << 16;
-        unsigned cum = 0;
-        for (int k = 0; k < s; ++k) {  // boundaries on 64 KiB multiples, never an empty window
-            cum += wt[k];
-            size_t b = k + 1 == s ? sh.len
-                                  : (sh.len / total * cum + sh.len % total * cum / total + kAlign / 2) / kAlign * kAlign;
-            if (b > sh.len) b = sh.len;
-            if (b > st.at[st.n]) st.at[++st.n] = b;
-        }
-        if (st.n == 0) st = Steps::one(sh.len, 0);
+        st.n = pipeline_windows(sh.len, s, taper(), st.at);
         st.piece = piece_for((in_bytes + static_cast<size_t>(n) * sh.rows * sh.len) / st.n);
         return st;
     }

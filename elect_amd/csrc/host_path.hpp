@@ -55,6 +55,9 @@ int device_numa_node(int dev);  // elect_ec_device_numa_node (-1: unknown)
 // The device a thread on NUMA node thread_node gets (host_device's choice; load: threads per listed device)
 int numa_pick(const int* devices, const int* nodes, int ndev, int thread_node, unsigned* load);
 int host_device_map(const int* devices, const int* nodes, int ndev, const int* thread_nodes, int nthreads, int* out);
+// The windows a pipelined batch of units of len bytes runs over in (at most) steps steps:
+// window k is [at[k], at[k + 1]); returns their number n (at[0] = 0, at[n] = len).  at: steps + 1 entries.
+int pipeline_windows(size_t len, int steps, bool taper, size_t* at);
 int set_batching(int enable, unsigned window_us, size_t arena_bytes);
 int host_path_stats(uint64_t* out, int n);  // elect_ec_host_path_stats
 int host_alloc(size_t bytes, void** out);    // elect_ec_host_alloc

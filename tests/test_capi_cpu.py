@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     assert len(declared) >= 17
     for name in declared:
         assert hasattr(_lib.lib, name), f"{name} missing from libelect_ec.so"
-    bound = {n for n, _, _ in _lib.SIGNATURES}
+    bound = {n for n, _, _ in _lib.SIGNATURES if not n.startswith("elect_ec_internal_")}  # (test hooks)
     assert bound == set(declared), "ctypes bindings out of sync with the header"
 
 
@@ -317,3 +317,27 @@ def test_numa_device_map():
     counts = [got.count(d) for d in devs]
     assert max(counts) - min(counts) <= 1, counts
     assert sum(nodes[d] == x for d, x in zip(got, mixed)) == 56
+
+
+def test_pipeline_windows():
+    """The windows a lone call is pipelined over (host_path.cpp pipeline_windows):
+    they cover [0, len) in order with no empty window, inner boundaries on 64 KiB multiples, at
+    most `steps` of them; tapered 4 : ... : 4 : 2 : 1, so the last window (the scatter left after
+    the last gather) is the smallest.  ELECT's codeLength in 5 steps: the plan DESIGN quotes."""
+    from elect_amd import _lib
+    K64 = 1 << 16
+    assert _lib.pipeline_windows(4404020, 5) == [0, 1179648, 2359296, 3538944, 4128768, 4404020]
+    for length in (1, 4095, K64, (1 << 20) - 7, 1 << 20, 4404020, 3 << 20, 17 << 20, (64 << 20) + 5):
+        for steps in range(1, 9):
+            for taper in (True, False):
+                at = _lib.pipeline_windows(length, steps, taper)
+                n = len(at) - 1
+                assert at[0] == 0 and at[-1] == length and 1 <= n <= steps, (length, steps, taper, at)
+                assert all(a < b for a, b in zip(at, at[1:])), (length, steps, taper, at)
+                assert all(b % K64 == 0 for b in at[1:-1]), (length, steps, taper, at)
+                w = [b - a for a, b in zip(at, at[1:])]
+                if taper and n == steps >= 3 and length >= steps * (1 << 20):
+                    assert w[-1] < w[-2] < w[0], (length, steps, w)
+                if not taper and n == steps and length >= steps * (1 << 20):
+                    assert max(w) - min(w) <= K64 * 2, (length, steps, w)  # equal up to the 64 KiB rounding
+    assert _lib.pipeline_windows(0, 3) == [0, 0]
