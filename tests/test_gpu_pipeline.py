@@ -116,6 +116,11 @@ CONFIGS = {
     "eight_steps_64k_pieces": {"ELECT_EC_PIPELINE_STEPS": "8", "ELECT_EC_STEP_KB": "256", "ELECT_EC_PIECE_KB": "64"},
     "eight_steps_16k_pieces": {"ELECT_EC_PIPELINE_STEPS": "8", "ELECT_EC_STEP_KB": "256", "ELECT_EC_PIECE_KB": "16"},
     "five_equal_windows_whole_table": {"ELECT_EC_PIPELINE_STEPS": "5", "ELECT_EC_TAPER": "0", "ELECT_EC_STAGE_WRITES": "0"},
+    # round 5's scheduling: no early issue (no gate counter waits), coarse polls, the default timer slack
+    "no_early_issue_coarse_polls": {"ELECT_EC_EARLY_ISSUE": "0", "ELECT_EC_POLL_FINE_US": "0",
+                                    "ELECT_EC_TIMER_SLACK_NS": "0"},
+    # early issue with a lead longer than a batch: every batch waits on the device for the previous one
+    "early_issue_long_lead": {"ELECT_EC_EARLY_US": "5000"},
 }
 
 
